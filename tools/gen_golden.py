@@ -1,0 +1,316 @@
+"""Generate golden vectors by running the REFERENCE sampler (/root/reference/gibbs.py).
+
+Runs only in the build container (the reference never travels).  Outputs small .npz
+fixtures under tests/golden/ that pin both the CPU oracle and the HIP path:
+
+* the reference's chain arrays (chain, bchain, zchain, poutchain, thetachain, alphachain,
+  dfchain) for a short run per run_sims.py model (run_sims.py:89-107), seeded;
+* the variate tape each sweep consumed (MH uniforms / index / jump / accept uniforms,
+  b normals, beta value, binomial uniforms, gamma values, dof-choice uniform), recovered
+  from the legacy MT19937 state around each call;
+* every likelihood evaluation (x, value) of the white and hyper MH blocks;
+* for each b draw: the reference's SVD mean, its draw term Li @ xi, the Cholesky mean
+  ``cho_solve(cho_factor(Sigma), d)`` (gibbs.py:321-322) and cond(Sigma).
+
+The only shim is Python-2 ``map`` -> list, set on the imported
+module; nothing of the reference is copied.
+"""
+from __future__ import annotations
+
+import builtins
+import os
+import sys
+import warnings
+
+import numpy as np
+import scipy.linalg as sl
+import scipy.stats
+
+sys.dont_write_bytecode = True
+sys.path.insert(0, "/root/reference")
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, ROOT)
+
+import gibbs as refgibbs  # noqa: E402  (the reference)
+
+from gibbs_student_t_amd import data as gdata  # noqa: E402
+from gibbs_student_t_amd.model import PTA  # noqa: E402
+
+refgibbs.map = lambda f, *a: list(builtins.map(f, *a))
+warnings.filterwarnings("ignore", category=DeprecationWarning)
+
+OUTDIR = os.path.join(ROOT, "tests", "golden")
+RS = np.random.mtrand._rand
+
+MODELS = {
+    # run_sims.py:89-107
+    "vvh17": dict(model="vvh17", vary_df=False, theta_prior="uniform", vary_alpha=False,
+                  alpha=1e10, pspin=0.00457),
+    "uniform": dict(model="mixture", vary_df=True, theta_prior="uniform"),
+    "beta": dict(model="mixture", vary_df=True, theta_prior="beta"),
+    "gaussian": dict(model="gaussian", vary_df=True, theta_prior="beta"),
+    "t": dict(model="t", vary_df=True, theta_prior="beta"),
+}
+
+
+def _same_state(a, b):
+    return (a[0] == b[0] and np.array_equal(a[1], b[1]) and a[2] == b[2]
+            and a[3] == b[3] and a[4] == b[4])
+
+
+class Rec:
+    stage = None
+    sweeps = []
+
+    @classmethod
+    def cur(cls):
+        return cls.sweeps[-1]
+
+
+_orig = {
+    "choice": np.random.choice, "randn": np.random.randn, "rand": np.random.rand,
+    "beta": scipy.stats.beta.rvs, "binom": scipy.stats.binom.rvs,
+    "gamma": scipy.stats.gamma.rvs,
+}
+
+
+def _uniform_of(call, *a, **k):
+    """Run ``call`` and recover the single uniform it consumed from the MT state."""
+    st0 = RS.get_state()
+    val = call(*a, **k)
+    st1 = RS.get_state()
+    RS.set_state(st0)
+    u = RS.random_sample()
+    assert _same_state(RS.get_state(), st1), "call consumed more than one uniform"
+    return val, u
+
+
+def rec_choice(a, size=None, replace=True, p=None):
+    ev = Rec.cur()
+    if p is not None:
+        val, u = _uniform_of(_orig["choice"], a, size=size, replace=replace, p=p)
+        if Rec.stage == "df":
+            ev["df_u"] = u
+        else:
+            ev[f"{Rec.stage}_u"].append(u)
+        return val
+    val = _orig["choice"](a, size=size, replace=replace, p=p)
+    ev[f"{Rec.stage}_idx"].append(int(np.asarray(val).ravel()[0]))
+    return val
+
+
+def rec_randn(*shape):
+    val = _orig["randn"](*shape)
+    ev = Rec.cur()
+    if Rec.stage in ("white", "hyper"):
+        ev[f"{Rec.stage}_xi"].append(float(val[0]))
+    elif Rec.stage == "b":
+        ev["b_xi"] = np.array(val)
+    return val
+
+
+def rec_rand(*shape):
+    val = _orig["rand"](*shape)
+    Rec.cur()[f"{Rec.stage}_acc"].append(float(val))
+    return val
+
+
+def rec_beta(*a, **k):
+    val = _orig["beta"](*a, **k)
+    Rec.cur()["beta"] = float(val)
+    return val
+
+
+def rec_binom(nn, p, *a, **k):
+    st0 = RS.get_state()
+    z = _orig["binom"](nn, p, *a, **k)
+    st1 = RS.get_state()
+    RS.set_state(st0)
+    p = np.asarray(p, dtype=np.float64)
+    u = np.full(len(p), np.nan)
+    for i, pi in enumerate(p):
+        if pi != 0.0:
+            u[i] = RS.random_sample()
+    assert _same_state(RS.get_state(), st1), "binomial uniform recovery failed"
+    RS.set_state(st1)
+    Rec.cur()["z_u"] = u
+    return z
+
+
+def rec_gamma(*a, **k):
+    val = _orig["gamma"](*a, **k)
+    Rec.cur()["gamma"] = np.array(val, dtype=np.float64)
+    return val
+
+
+class RecordingGibbs(refgibbs.Gibbs):
+    def update_white_params(self, xs):
+        Rec.sweeps.append({k: [] for k in ("white_u", "white_idx", "white_xi", "white_acc",
+                                          "hyper_u", "hyper_idx", "hyper_xi", "hyper_acc",
+                                          "white_lnl_x", "white_lnl", "hyper_lnl_x",
+                                          "hyper_lnl")})
+        Rec.stage = "white"
+        out = super().update_white_params(xs)
+        Rec.cur()["x_white"] = np.array(out)
+        return out
+
+    def update_hyper_params(self, xs):
+        Rec.stage = "hyper"
+        return super().update_hyper_params(xs)
+
+    def update_b(self, xs):
+        Rec.stage = "b"
+        b = super().update_b(xs)
+        params = self.map_params(xs)
+        phiinv = self.pta.get_phiinv(params, logdet=False)[0]
+        Sigma = self.TNT + np.diag(phiinv)
+        u, s, _ = sl.svd(Sigma)
+        mn = np.dot(u, np.dot(u.T, self.d) / s)
+        Li = u * np.sqrt(1 / s)
+        ev = Rec.cur()
+        ev["b_delta"] = np.dot(Li, ev["b_xi"])
+        ev["b_mean_svd"] = mn
+        ev["b_mean_chol"] = sl.cho_solve(sl.cho_factor(Sigma), self.d)
+        ev["b_cond"] = float(np.linalg.cond(Sigma))
+        ev["b_ref"] = np.array(b)
+        assert np.array_equal(b, mn + np.dot(Li, ev["b_xi"]))
+        return b
+
+    def update_theta(self, xs):
+        Rec.stage = "theta"
+        return super().update_theta(xs)
+
+    def update_z(self, xs):
+        Rec.stage = "z"
+        return super().update_z(xs)
+
+    def update_alpha(self, xs):
+        Rec.stage = "alpha"
+        return super().update_alpha(xs)
+
+    def update_df(self, xs):
+        Rec.stage = "df"
+        return super().update_df(xs)
+
+    def get_lnlikelihood_white(self, xs):
+        v = super().get_lnlikelihood_white(xs)
+        ev = Rec.cur()
+        ev["white_lnl_x"].append(np.array(xs, dtype=np.float64))
+        ev["white_lnl"].append(float(v))
+        return v
+
+    def get_lnlikelihood(self, xs):
+        v = super().get_lnlikelihood(xs)
+        ev = Rec.cur()
+        ev["hyper_lnl_x"].append(np.array(xs, dtype=np.float64))
+        ev["hyper_lnl"].append(float(v))
+        return v
+
+
+def _install():
+    np.random.choice = rec_choice
+    np.random.randn = rec_randn
+    np.random.rand = rec_rand
+    scipy.stats.beta.rvs = rec_beta
+    scipy.stats.binom.rvs = rec_binom
+    scipy.stats.gamma.rvs = rec_gamma
+
+
+def _uninstall():
+    np.random.choice = _orig["choice"]
+    np.random.randn = _orig["randn"]
+    np.random.rand = _orig["rand"]
+    for nm in ("beta", "binom", "gamma"):
+        if nm in getattr(scipy.stats, nm).__dict__:
+            del getattr(scipy.stats, nm).__dict__["rvs"]
+
+
+def pack_tape(sweeps, n, m, P):
+    S = len(sweeps)
+    T = {
+        "white_u": np.full((S, 20), np.nan), "white_idx": np.full((S, 20), -1, np.int64),
+        "white_xi": np.full((S, 20), np.nan), "white_acc": np.full((S, 20), np.nan),
+        "hyper_u": np.full((S, 10), np.nan), "hyper_idx": np.full((S, 10), -1, np.int64),
+        "hyper_xi": np.full((S, 10), np.nan), "hyper_acc": np.full((S, 10), np.nan),
+        "b_xi": np.full((S, m), np.nan), "b_delta": np.full((S, m), np.nan),
+        "b_mean_svd": np.full((S, m), np.nan), "b_mean_chol": np.full((S, m), np.nan),
+        "b_ref": np.full((S, m), np.nan), "b_cond": np.full(S, np.nan),
+        "beta": np.full(S, np.nan), "z_u": np.full((S, n), np.nan),
+        "gamma": np.full((S, n), np.nan), "df_u": np.full(S, np.nan),
+        "x_white": np.full((S, P), np.nan),
+        "white_lnl_x": np.full((S, 21, P), np.nan), "white_lnl": np.full((S, 21), np.nan),
+        "hyper_lnl_x": np.full((S, 11, P), np.nan), "hyper_lnl": np.full((S, 11), np.nan),
+    }
+    for i, ev in enumerate(sweeps):
+        for stage, k in (("white", 20), ("hyper", 10)):
+            T[f"{stage}_u"][i] = ev[f"{stage}_u"]
+            T[f"{stage}_xi"][i] = ev[f"{stage}_xi"]
+            T[f"{stage}_acc"][i] = ev[f"{stage}_acc"]
+            T[f"{stage}_idx"][i] = ev[f"{stage}_idx"]
+            T[f"{stage}_lnl_x"][i] = np.array(ev[f"{stage}_lnl_x"])
+            T[f"{stage}_lnl"][i] = ev[f"{stage}_lnl"]
+        T["x_white"][i] = ev["x_white"]
+        for key in ("b_xi", "b_delta", "b_mean_svd", "b_mean_chol", "b_ref", "b_cond",
+                    "beta", "z_u", "gamma", "df_u"):
+            if key in ev:
+                T[key][i] = ev[key]
+    return T
+
+
+def run_one(pta, name, kw, seed, niter, x0=None):
+    Rec.sweeps = []
+    np.random.seed(seed)
+    xs = pta.sample_params() if x0 is None else np.array(x0, dtype=np.float64)
+    g = RecordingGibbs(pta, **kw)
+    _install()
+    try:
+        g.sample(xs, niter=niter)
+    finally:
+        _uninstall()
+    n, m, P = pta.n, pta.m, len(xs)
+    tape = pack_tape(Rec.sweeps, n, m, P)
+    out = dict(xs=xs, seed=seed, niter=niter, chain=g.chain, bchain=g.bchain,
+               zchain=g.zchain, poutchain=g.poutchain, thetachain=g.thetachain,
+               alphachain=g.alphachain, dfchain=g.dfchain,
+               final_b=g._b, final_z=np.asarray(g._z, dtype=np.float64),
+               final_alpha=g._alpha, final_pout=g._pout, final_theta=g._theta,
+               final_df=float(g.tdf), prior_draw=int(x0 is None))
+    out.update({f"tape_{k}": v for k, v in tape.items()})
+    return out
+
+
+def dataset_arrays(pta, psr):
+    return dict(toas=psr.toas, residuals=psr.residuals, toaerrs=psr.toaerrs, Mmat=psr.Mmat,
+                T=pta.T, Ffreqs=pta.Ffreqs, components=pta.components,
+                tm_weight=pta.tm_weight, names=np.array(pta.param_names))
+
+
+def main():
+    os.makedirs(OUTDIR, exist_ok=True)
+    niter = 12
+    psr = gdata.j1713(seed=1713, theta=0.05)
+    pta = PTA(psr)
+    np.savez_compressed(os.path.join(OUTDIR, "j1713_dataset.npz"), **dataset_arrays(pta, psr))
+    for i, (name, kw) in enumerate(MODELS.items()):
+        for tag, x0 in (("prior", None), ("fixed", [4.33, -14.0, -7.6])):
+            out = run_one(pta, name, kw, seed=1000 + 17 * i + (tag == "fixed"),
+                          niter=niter, x0=x0)
+            out["model_kw"] = np.array(repr(kw))
+            fn = os.path.join(OUTDIR, f"ref_{name}_{tag}.npz")
+            np.savez_compressed(fn, **out)
+            print(name, tag, "cond(b):", np.nanmax(out["tape_b_cond"]),
+                  "redraws:", int(np.sum(~np.isnan(out["tape_b_cond"]))), file=sys.stderr)
+    # varied efac (notebook-style, gibbs_likelihood.ipynb cell 2): two white parameters,
+    # so the white index draw is exercised
+    pta2 = PTA(psr, efac=(0.2, 10.0))
+    np.savez_compressed(os.path.join(OUTDIR, "j1713_dataset_efac.npz"),
+                        **dataset_arrays(pta2, psr))
+    out = run_one(pta2, "beta", MODELS["beta"], seed=4242, niter=niter,
+                  x0=[1.1, 4.33, -14.0, -7.6])
+    out["model_kw"] = np.array(repr(MODELS["beta"]))
+    np.savez_compressed(os.path.join(OUTDIR, "ref_beta_efac_fixed.npz"), **out)
+    print("efac fixed cond:", np.nanmax(out["tape_b_cond"]), file=sys.stderr)
+
+
+if __name__ == "__main__":
+    main()
