@@ -1,0 +1,225 @@
+"""Benchmark: aggregate Gibbs sweeps/s (+ ESS/s) on J1713+0747, batched chains per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--chains C]
+
+A *step* is one Gibbs sweep (gibbs.py:354-380) of every chain on every rank.  Each rank
+owns C chains (weak scaling, default 1024 = BASELINE config 2 per GPU) of the run_sims.py
+'beta' outlier-mixture model (run_sims.py:98-99) on J1713+0747's 130 TOAs; the timed region
+is exactly K sweeps in one persistent launch, recording every sweep's full state (chain,
+bchain, zchain, alphachain, poutchain, thetachain, dfchain) to HBM as the reference records
+every sweep.  For N > 1 the driver starts one process per GPU with torch.distributed.run;
+chains never communicate while sampling, the only collective is the final summary
+all-reduce (RCCL).  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Gibbs sweeps/sec (node aggregate) + ESS/sec, J1713+0747, 1/2/4/8 GPU"
+FP64_PEAK_TFLOPS = 78.6      # MI355X fp64 matrix (= vector) dense peak, AMD spec
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+CFG = dict(model="mixture", vary_df=True, theta_prior="beta")   # run_sims.py:98-99
+
+
+def algorithmic_flops(n: int, m: int) -> float:
+    """Fixed work per chain-sweep: Gram of [T|r], 12 Cholesky (11 MH + 1
+    draw), 12 pairs of triangular solves, one T b."""
+    return n * (m + 1) * (m + 2) + 12 * m ** 3 / 3 + 12 * 4 * m ** 2 + 2 * n * m
+
+
+def toa_pass_bytes(n: int) -> float:
+    """Per-TOA pass HBM bytes per chain-sweep: 8 n (6 + 2*21)."""
+    return 8.0 * n * (6 + 2 * 21)
+
+
+# ------------------------------------------------------------------------------------------
+# CPU baseline: the oracle (a faithful port of gibbs.py, bit-exact to the reference on the
+# same MT19937 stream) timed on host cores, one chain per single-threaded process.
+# ------------------------------------------------------------------------------------------
+def _cpu_worker(seconds: float, seed: int):
+    import warnings
+
+    from gibbs_student_t_amd import data
+    from gibbs_student_t_amd.model import PTA
+    from oracle.gibbs_oracle import (LegacyNumpyVariates, Oracle, OutlierModel,
+                                     initial_state)
+    warnings.simplefilter("ignore")
+    pta = PTA(data.j1713())
+    orc = Oracle(pta, OutlierModel(**CFG))
+    np.random.seed(seed)
+    x = pta.sample_params()
+    st = initial_state(pta, orc.cfg)
+    src = LegacyNumpyVariates()
+    for _ in range(3):
+        x = orc.sweep(st, x, src)
+    t0 = time.perf_counter()
+    k = 0
+    while time.perf_counter() - t0 < seconds:
+        x = orc.sweep(st, x, src)
+        k += 1
+    print(json.dumps({"sweeps": k, "seconds": time.perf_counter() - t0}))
+
+
+def cpu_baseline(seconds: float, cores: int):
+    env = dict(os.environ, OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1",
+               MKL_NUM_THREADS="1", HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker",
+                               str(seconds), str(1000 + i)], env=env, stdout=subprocess.PIPE,
+                              stderr=subprocess.DEVNULL, text=True) for i in range(cores)]
+    tot = 0.0
+    sweeps = 0
+    for p in procs:
+        out, _ = p.communicate(timeout=seconds * 10 + 120)
+        r = json.loads(out.strip().splitlines()[-1])
+        tot += r["sweeps"] / r["seconds"]
+        sweeps += r["sweeps"]
+    return {"value": tot, "unit": "chain-sweeps/s", "cores": cores, "kind": "port",
+            "sample": f"{cores} single-thread processes x {seconds:.0f} s of the oracle "
+                      f"(oracle/gibbs_oracle.py, numpy legacy RNG, bit-exact to gibbs.py), "
+                      f"one J1713 mixture chain each, {sweeps} sweeps total"}
+
+
+# ------------------------------------------------------------------------------------------
+def initial_state(pta, C: int, chain0: int):
+    """Prior draws per global chain id (run_sims.py:111) and the gibbs.py:29-51 latents."""
+    n, m = pta.T.shape
+    lo = np.array([p.pmin for p in pta.params])
+    hi = np.array([p.pmax for p in pta.params])
+    x = np.stack([np.random.default_rng([7, chain0 + c]).uniform(lo, hi) for c in range(C)])
+    return dict(x=x, b=np.zeros((C, m)), z=np.ones((C, n)), alpha=np.ones((C, n)),
+                pout=np.zeros((C, n)), theta=np.full(C, 0.01), nu=np.full(C, 4.0))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=300)
+    ap.add_argument("--chains", type=int, default=1024, help="chains per GPU")
+    ap.add_argument("--seed", type=int, default=20171713)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-worker", nargs=2, default=None)
+    args = ap.parse_args()
+    if args.cpu_worker:
+        _cpu_worker(float(args.cpu_worker[0]), int(args.cpu_worker[1]))
+        return
+
+    from gibbs_student_t_amd import dist
+    rank, local, world = dist.env_rank()
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cores = max(1, min(16, os.cpu_count() or 1))
+        cpu = cpu_baseline(args.cpu_seconds, cores)      # before the GPU is touched
+
+    import torch
+    from gibbs_student_t_amd import data, diag
+    from gibbs_student_t_amd.model import PTA
+    from gibbs_student_t_amd.native import NativeSampler
+
+    rank, local, world = dist.init()
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    pta = PTA(data.j1713())
+    n, m = pta.T.shape
+    C, K, W = args.chains, args.steps, args.warmup
+    c0, _ = dist.chain_range(rank, C)
+    ns = NativeSampler(pta, CFG, local)
+    ns.alloc(C)
+    ns.set_state(**initial_state(pta, C, c0))
+    if W > 0:
+        ns.sweep(W, seed=args.seed, sweep0=0, chain0=c0)
+    rec = ns.alloc_records(K)
+    torch.cuda.synchronize(dev)
+    dist.barrier(dev)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ns.sweep(K, records=rec, seed=args.seed, sweep0=W, chain0=c0)
+    torch.cuda.synchronize(dev)
+    dist.barrier(dev)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kernel_ms = ns.last_kernel_ms()
+    status = ns.get_state()["status"]
+
+    # ESS over this rank's chains, then summed over ranks (disjoint chain sets)
+    xs = rec["x"].cpu().numpy()
+    th = rec["theta"].cpu().numpy()
+    names = [p.name.split("_", 1)[1] for p in pta.params]
+    series = {nm: xs[:, :, j] for j, nm in enumerate(names)}
+    series["theta"] = th
+    ess = {k: diag.bulk_ess(v) for k, v in series.items()}
+    rhat = {k: diag.split_rhat(v) for k, v in series.items()}
+    keys = list(series)
+    s_vec = np.array([ess[k] for k in keys] + [float((status != 0).sum())])
+    m_vec = np.array([elapsed, kernel_ms] + [rhat[k] for k in keys])
+    s_vec, m_vec = dist.reduce_summary(s_vec, m_vec, dev)
+    elapsed, kernel_ms = float(m_vec[0]), float(m_vec[1])
+    ess_tot = dict(zip(keys, s_vec[:len(keys)]))
+    rhat_max = dict(zip(keys, m_vec[2:]))
+
+    if rank == 0:
+        total = C * world * K
+        value = total / elapsed
+        flops = algorithmic_flops(n, m) * C * K
+        achieved = flops / (kernel_ms * 1e-3) / 1e12
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            try:
+                pj = json.load(open(pmc))
+                traffic = pj["hbm_bytes_per_chain_sweep"] * C * K
+            except Exception:
+                traffic = None
+        min_ess = float(min(ess_tot.values()))
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "chain-sweeps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": elapsed / K * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic residuals at the 130 real J1713+0747 TOA epochs "
+                    "(white + power-law red + 5% outliers, seeded); chains start from prior "
+                    "draws",
+            "config": {"workload": "J1713+0747 Student-t/outlier-mixture Gibbs sampler "
+                                   "(run_sims 'beta' model), fp64",
+                       "chains_per_gpu": C, "chains_total": C * world, "n_toa": n,
+                       "basis_cols": m, "record_every": 1,
+                       "parallelism": f"independent chains sharded over {world} GPU(s); "
+                                      "RCCL only for the final summary all-reduce"},
+            "ess_per_sec": min_ess / elapsed,
+            "ess_total": {k: float(v) for k, v in ess_tot.items()},
+            "rhat_max": {k: float(v) for k, v in rhat_max.items()},
+            "chains_with_status": int(s_vec[-1]),
+            "kernel_ms": kernel_ms,
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
+                         "traffic": traffic,
+                         "algorithmic_flop_per_chain_sweep": algorithmic_flops(n, m),
+                         "toa_pass_GBps": toa_pass_bytes(n) * C * K / (kernel_ms * 1e-3)
+                         / 1e9},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    ns.close()
+    dist.finalize()
+
+
+if __name__ == "__main__":
+    main()

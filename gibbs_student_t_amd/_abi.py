@@ -1,0 +1,123 @@
+"""ctypes binding of libgst.so (C ABI declared in include/gst.h).
+
+The product path has no CPU fallback: if the shared library is missing or cannot be
+loaded, ``load()`` raises ``GstNativeError``.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgst.so")
+
+GST_MODEL_GAUSSIAN, GST_MODEL_T, GST_MODEL_MIXTURE, GST_MODEL_VVH17 = 0, 1, 2, 3
+STAGE_WHITE, STAGE_HYPER, STAGE_B = 1, 2, 4
+STAGE_THETA, STAGE_Z, STAGE_ALPHA, STAGE_DF = 8, 16, 32, 64
+STAGE_ALL = 0x7F
+STAGE_B_FORCE = 0x80
+TAPE_WHITE, TAPE_HYPER, TAPE_DELTA = 0, 80, 120
+
+EXPORTS = ("gst_version", "gst_tape_stride", "gst_last_error", "gst_ctx_create",
+           "gst_ctx_destroy", "gst_model_set", "gst_sweep", "gst_eval_lnlike", "gst_sync",
+           "gst_last_sweep_ms", "gst_debug_stamps")
+
+_P = ct.POINTER
+_D = _P(ct.c_double)
+_I = _P(ct.c_int)
+
+
+class GstNativeError(RuntimeError):
+    pass
+
+
+class ModelDesc(ct.Structure):
+    _fields_ = [
+        ("n", ct.c_int), ("m", ct.c_int), ("nfourier", ct.c_int), ("ntm", ct.c_int),
+        ("nparams", ct.c_int),
+        ("T", _D), ("residuals", _D), ("toaerrs", _D), ("ffreqs", _D),
+        ("tm_weight", ct.c_double),
+        ("idx_efac", ct.c_int), ("idx_equad", ct.c_int), ("idx_log10_A", ct.c_int),
+        ("idx_gamma", ct.c_int),
+        ("efac_const", ct.c_double),
+        ("pmin", _D), ("pmax", _D),
+        ("hyper_idx", _I), ("n_hyper", ct.c_int), ("white_idx", _I), ("n_white", ct.c_int),
+        ("model", ct.c_int), ("vary_df", ct.c_int), ("vary_alpha", ct.c_int),
+        ("theta_prior_beta", ct.c_int), ("mprior", ct.c_double), ("pspin", ct.c_double),
+        ("df_A", _D), ("df_B", _D),
+    ]
+
+
+class State(ct.Structure):
+    _fields_ = [("x", ct.c_void_p), ("b", ct.c_void_p), ("z", ct.c_void_p),
+                ("alpha", ct.c_void_p), ("pout", ct.c_void_p), ("theta", ct.c_void_p),
+                ("nu", ct.c_void_p), ("status", ct.c_void_p)]
+
+
+class Records(ct.Structure):
+    _fields_ = [("x", ct.c_void_p), ("b", ct.c_void_p), ("z", ct.c_void_p),
+                ("alpha", ct.c_void_p), ("pout", ct.c_void_p), ("theta", ct.c_void_p),
+                ("nu", ct.c_void_p), ("nrec", ct.c_int)]
+
+
+class Tape(ct.Structure):
+    _fields_ = [("data", ct.c_void_p), ("stride", ct.c_int)]
+
+
+_lib = None
+
+
+def load(path: str | None = None):
+    """Load libgst.so once; raise GstNativeError if it is absent or broken."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or os.environ.get("GST_LIB", LIB_PATH)
+    # PyTorch owns the device buffers: its HIP runtime must be the one libgst binds to
+    # (same soname libamdhip64.so.7), so import it before dlopen-ing the library.
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # pragma: no cover
+        pass
+    if not os.path.exists(p):
+        raise GstNativeError(
+            f"native library {p} not found: build it with `python __graft_entry__.py` "
+            "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    try:
+        lib = ct.CDLL(p)
+    except OSError as e:  # pragma: no cover - depends on the machine
+        raise GstNativeError(f"cannot load {p}: {e}") from e
+    for name in EXPORTS:
+        if not hasattr(lib, name):
+            raise GstNativeError(f"{p} lacks symbol {name}")
+    lib.gst_version.restype = ct.c_int
+    lib.gst_tape_stride.argtypes = [ct.c_int, ct.c_int]
+    lib.gst_last_error.argtypes = [ct.c_char_p, ct.c_size_t]
+    lib.gst_ctx_create.argtypes = [ct.c_int, _P(ct.c_void_p)]
+    lib.gst_ctx_destroy.argtypes = [ct.c_void_p]
+    lib.gst_model_set.argtypes = [ct.c_void_p, _P(ModelDesc)]
+    lib.gst_sweep.argtypes = [ct.c_void_p, _P(State), _P(Records), _P(Tape), ct.c_int,
+                              ct.c_int, ct.c_longlong, ct.c_int, ct.c_uint, ct.c_ulonglong,
+                              ct.c_longlong, ct.c_void_p]
+    lib.gst_eval_lnlike.argtypes = [ct.c_void_p, _P(State), ct.c_int, ct.c_void_p,
+                                    ct.c_void_p, ct.c_void_p]
+    lib.gst_sync.argtypes = [ct.c_void_p, ct.c_void_p]
+    lib.gst_last_sweep_ms.argtypes = [ct.c_void_p, _P(ct.c_double)]
+    lib.gst_debug_stamps.argtypes = [ct.c_void_p, ct.c_void_p]
+    for name in EXPORTS:
+        if name != "gst_version":
+            getattr(lib, name).restype = ct.c_int
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def last_error(lib) -> str:
+    buf = ct.create_string_buffer(1024)
+    lib.gst_last_error(buf, len(buf))
+    return buf.value.decode(errors="replace")
+
+
+def check(lib, rc: int, what: str):
+    if rc != 0:
+        raise GstNativeError(f"{what} failed: {last_error(lib)}")

@@ -1,0 +1,352 @@
+// C ABI of libgst.so (declared in include/gst.h): context, model upload, sweep launch.
+//
+// The host side only packs model constants into the layouts the kernel wants and picks
+// the template instance (matrix slots MT, TOA slots NS, timing-model panels K0, tape or
+// Philox variates).  All chain state lives in caller-owned device buffers.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "gst.h"
+#include "gst_kernel.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const std::string& msg) {
+  g_err = msg;
+  return -1;
+}
+
+#define HIP_OK(expr)                                                              \
+  do {                                                                            \
+    hipError_t e_ = (expr);                                                       \
+    if (e_ != hipSuccess)                                                         \
+      return fail(std::string(#expr) + ": " + hipGetErrorString(e_));             \
+  } while (0)
+
+struct Ctx {
+  int device = 0;
+  bool has_model = false;
+  gst::DevModel md{};
+  int MT = 0, NS = 0, K0 = 0, WPB = 4;
+  std::vector<void*> allocs;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+};
+
+int upload(Ctx* cx, const void* host, size_t bytes, void** dev) {
+  void* p = nullptr;
+  HIP_OK(hipMalloc(&p, bytes > 0 ? bytes : 16));
+  if (bytes) HIP_OK(hipMemcpy(p, host, bytes, hipMemcpyHostToDevice));
+  cx->allocs.push_back(p);
+  *dev = p;
+  return 0;
+}
+
+void free_model(Ctx* cx) {
+  for (void* p : cx->allocs) (void)hipFree(p);
+  cx->allocs.clear();
+  cx->has_model = false;
+}
+
+typedef void (*kfn_t)(const gst::DevModel, const gst::DevState, const gst::DevRec,
+                      const gst::DevTape, int, int, long long, int, unsigned,
+                      unsigned long long, long long, int, double*, double*);
+
+template <int MT, int NS, int K0, bool TAPE>
+kfn_t kfn() {
+  return &gst::gst_sweep_kernel<MT, NS, K0, TAPE>;
+}
+
+// Instantiated shapes: MT = padded matrix dim / 8, NS = TOA slots of 64, K0 = TM panels.
+kfn_t pick(int MT, int NS, int K0, bool tape) {
+#define GST_CASE(mt, ns, k0)                                             \
+  if (MT == mt && NS == ns && K0 == k0)                                  \
+    return tape ? kfn<mt, ns, k0, true>() : kfn<mt, ns, k0, false>();
+  GST_CASE(10, 3, 2)
+  GST_CASE(10, 4, 2)
+  GST_CASE(12, 4, 2)
+#undef GST_CASE
+  return nullptr;
+}
+
+int round_up(int a, int b) { return (a + b - 1) / b * b; }
+
+}  // namespace
+
+extern "C" {
+
+int gst_version(void) { return GST_ABI_VERSION; }
+
+int gst_tape_stride(int n, int m) { return gst::TP_DELTA + m + 2 + 2 * n; }
+
+int gst_last_error(char* buf, size_t len) {
+  if (!buf || !len) return -1;
+  std::snprintf(buf, len, "%s", g_err.c_str());
+  return 0;
+}
+
+int gst_ctx_create(int device, void** ctx) {
+  if (!ctx) return fail("gst_ctx_create: null ctx");
+  int ndev = 0;
+  HIP_OK(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail("gst_ctx_create: bad device index");
+  HIP_OK(hipSetDevice(device));
+  Ctx* cx = new Ctx();
+  cx->device = device;
+  HIP_OK(hipEventCreate(&cx->ev0));
+  HIP_OK(hipEventCreate(&cx->ev1));
+  *ctx = cx;
+  return 0;
+}
+
+int gst_ctx_destroy(void* ctx) {
+  Ctx* cx = static_cast<Ctx*>(ctx);
+  if (!cx) return 0;
+  (void)hipSetDevice(cx->device);
+  free_model(cx);
+  if (cx->ev0) (void)hipEventDestroy(cx->ev0);
+  if (cx->ev1) (void)hipEventDestroy(cx->ev1);
+  delete cx;
+  return 0;
+}
+
+int gst_model_set(void* ctx, const gst_model_desc* d) {
+  Ctx* cx = static_cast<Ctx*>(ctx);
+  if (!cx || !d) return fail("gst_model_set: null argument");
+  HIP_OK(hipSetDevice(cx->device));
+  const int n = d->n, m = d->m, nf = d->nfourier, ntm = d->ntm, P = d->nparams;
+  if (n <= 0 || m != nf + ntm || nf <= 0 || ntm < 0) return fail("gst_model_set: bad sizes");
+  if (P < 1 || P > 4) return fail("gst_model_set: nparams must be 1..4");
+  if (d->idx_equad < 0 || d->idx_log10_A < 0 || d->idx_gamma < 0)
+    return fail("gst_model_set: equad, log10_A and gamma parameters are required");
+  if (d->n_hyper < 1 || d->n_hyper > 4 || d->n_white < 1 || d->n_white > 4)
+    return fail("gst_model_set: bad hyper/white index sets");
+  const int ntm_pad = round_up(ntm > 0 ? ntm : 1, 8);
+  const int raug = ntm_pad + nf;
+  const int mpad = round_up(raug + 1, 16);
+  const int MT = mpad / 8, K0 = ntm_pad / 8;
+  const int NS = (n + 63) / 64 <= 3 ? 3 : 4;
+  const int npad = 64 * ((n + 63) / 64);
+  if (round_up(n, 4) > 64 * NS) return fail("gst_model_set: n too large for TOA slots");
+  int MTk = MT;
+  if (!pick(MTk, NS, K0, false)) {
+    if (MT <= 12 && pick(12, 4, K0, false)) {
+      return fail("gst_model_set: internal: unsupported padded shape");
+    }
+    char b[160];
+    std::snprintf(b, sizeof b,
+                  "gst_model_set: no kernel instance for MT=%d NS=%d K0=%d (n=%d m=%d)", MT,
+                  NS, K0, n, m);
+    return fail(b);
+  }
+  free_model(cx);
+
+  // internal column order: [TM | pad | Fourier | r | pad]
+  std::vector<int> ref2int(m), int2ref(mpad, -1);
+  for (int j = 0; j < nf; ++j) ref2int[j] = ntm_pad + j;
+  for (int j = 0; j < ntm; ++j) ref2int[nf + j] = j;
+  for (int j = 0; j < m; ++j) int2ref[ref2int[j]] = j;
+  const int NT = mpad / 16;
+  const int nks = round_up(n, 4) / 4;
+  std::vector<double> Tmf((size_t)nks * NT * 64, 0.0);
+  for (int ks = 0; ks < nks; ++ks)
+    for (int X = 0; X < NT; ++X)
+      for (int l = 0; l < 64; ++l) {
+        const int t = 4 * ks + (l >> 4);
+        const int i = 16 * X + (l & 15);
+        double v = 0.0;
+        if (t < n) {
+          if (i == raug)
+            v = d->residuals[t];
+          else if (i < mpad && int2ref[i] >= 0)
+            v = d->T[(size_t)t * m + int2ref[i]];
+        }
+        Tmf[((size_t)ks * NT + X) * 64 + l] = v;
+      }
+  std::vector<double> Tcol((size_t)m * npad, 0.0), resid(npad, 0.0), sig2(npad, 0.0);
+  for (int t = 0; t < n; ++t) {
+    for (int j = 0; j < m; ++j) Tcol[(size_t)j * npad + t] = d->T[(size_t)t * m + j];
+    resid[t] = d->residuals[t];
+    sig2[t] = d->toaerrs[t] * d->toaerrs[t];
+  }
+  // red-noise spectrum pieces: log f_k and log df_k (df from f[::2], enterprise powerlaw)
+  std::vector<double> lf(nf), ldf(nf);
+  for (int k = 0; k < nf; ++k) {
+    lf[k] = std::log(d->ffreqs[k]);
+    const int pair = k / 2;
+    const double prev = pair == 0 ? 0.0 : d->ffreqs[2 * (pair - 1)];
+    ldf[k] = std::log(d->ffreqs[2 * pair] - prev);
+  }
+  std::vector<double> dfA(32, 0.0), dfB(32, 0.0);
+  for (int k = 0; k < 30; ++k) {
+    dfA[k] = d->df_A[k];
+    dfB[k] = d->df_B[k];
+  }
+
+  gst::DevModel md{};
+  void* ptr;
+  if (upload(cx, Tmf.data(), Tmf.size() * 8, &ptr)) return -1;
+  md.Tmf = (const double*)ptr;
+  if (upload(cx, Tcol.data(), Tcol.size() * 8, &ptr)) return -1;
+  md.Tcol = (const double*)ptr;
+  if (upload(cx, resid.data(), resid.size() * 8, &ptr)) return -1;
+  md.resid = (const double*)ptr;
+  if (upload(cx, sig2.data(), sig2.size() * 8, &ptr)) return -1;
+  md.sig2 = (const double*)ptr;
+  if (upload(cx, lf.data(), lf.size() * 8, &ptr)) return -1;
+  md.lfreq = (const double*)ptr;
+  if (upload(cx, ldf.data(), ldf.size() * 8, &ptr)) return -1;
+  md.ldf = (const double*)ptr;
+  if (upload(cx, dfA.data(), dfA.size() * 8, &ptr)) return -1;
+  md.dfA = (const double*)ptr;
+  if (upload(cx, dfB.data(), dfB.size() * 8, &ptr)) return -1;
+  md.dfB = (const double*)ptr;
+  if (upload(cx, ref2int.data(), ref2int.size() * sizeof(int), &ptr)) return -1;
+  md.ref2int = (const int*)ptr;
+
+  md.n = n;
+  md.m = m;
+  md.nf = nf;
+  md.ntm = ntm;
+  md.ntm_pad = ntm_pad;
+  md.raug = raug;
+  md.nks = nks;
+  md.npad = npad;
+  md.nslot_toa = npad / 64;
+  md.P = P;
+  md.idx_efac = d->idx_efac;
+  md.idx_equad = d->idx_equad;
+  md.idx_logA = d->idx_log10_A;
+  md.idx_gamma = d->idx_gamma;
+  md.efac_const = d->efac_const;
+  for (int j = 0; j < 4; ++j) {
+    md.pmin[j] = j < P ? d->pmin[j] : 0.0;
+    md.pmax[j] = j < P ? d->pmax[j] : 0.0;
+    md.lp_in[j] = j < P ? -std::log(d->pmax[j] - d->pmin[j]) : 0.0;
+    md.hind[j] = j < d->n_hyper ? d->hyper_idx[j] : d->hyper_idx[0];
+    md.wind[j] = j < d->n_white ? d->white_idx[j] : d->white_idx[0];
+  }
+  md.nh = d->n_hyper;
+  md.nw = d->n_white;
+  md.sig_h = 0.05 * d->n_hyper;
+  md.sig_w = 0.05 * d->n_white;
+  const double probs[5] = {0.1, 0.15, 0.5, 0.15, 0.1};
+  const double sizes[5] = {0.1, 0.5, 1.0, 3.0, 10.0};
+  double cs = 0.0, cdf[5];
+  for (int i = 0; i < 5; ++i) {
+    cs += probs[i];
+    cdf[i] = cs;
+  }
+  for (int i = 0; i < 5; ++i) {
+    md.mh_cdf[i] = cdf[i] / cdf[4];
+    md.mh_size[i] = sizes[i];
+  }
+  md.model = d->model;
+  md.vary_df = d->vary_df;
+  md.vary_alpha = d->vary_alpha;
+  if (d->theta_prior_beta) {
+    md.mk = n * d->mprior;
+    md.k1mm = n * (1.0 - d->mprior);
+  } else {
+    md.mk = 1.0;
+    md.k1mm = 1.0;
+  }
+  md.pspin = d->pspin;
+  md.tm_phiinv = 1.0 / d->tm_weight;
+  md.logdet_phi_tm = ntm * std::log(d->tm_weight);
+  md.log_fyr = std::log(1.0 / (365.25 * 86400.0));
+  md.log_12pi2 = std::log(12.0) + 2.0 * std::log(M_PI);
+  cx->md = md;
+  cx->MT = MT;
+  cx->NS = NS;
+  cx->K0 = K0;
+  cx->WPB = gst::wpb_for(MT, NS);
+  cx->has_model = true;
+  return 0;
+}
+
+static int launch(Ctx* cx, const gst_state* s, const gst_records* r, const gst_tape* tp,
+                  int C, int nsweeps, long long sweep0, int record_every, unsigned mask,
+                  unsigned long long seed, long long chain0, int eval_only, double* ow,
+                  double* oh, void* stream) {
+  if (!cx || !cx->has_model) return fail("gst: no model set");
+  if (!s || !s->x || !s->b || !s->z || !s->alpha || !s->pout || !s->theta || !s->nu)
+    return fail("gst: state pointers must all be set");
+  if (C <= 0) return 0;
+  HIP_OK(hipSetDevice(cx->device));
+  const bool tape = tp && tp->data;
+  kfn_t k = pick(cx->MT, cx->NS, cx->K0, tape);
+  if (!k) return fail("gst: no kernel instance");
+  gst::DevState ds{s->x, s->b, s->z, s->alpha, s->pout, s->theta, s->nu, s->status};
+  gst::DevRec dr{};
+  if (r) dr = gst::DevRec{r->x, r->b, r->z, r->alpha, r->pout, r->theta, r->nu, r->nrec};
+  else record_every = 0;
+  if (tape && tp->stride != gst_tape_stride(cx->md.n, cx->md.m))
+    return fail("gst: tape stride mismatch");
+  gst::DevTape dt{tape ? tp->data : nullptr, tape ? tp->stride : 0};
+  const dim3 grid((C + cx->WPB - 1) / cx->WPB), block(64 * cx->WPB);
+  hipStream_t st = (hipStream_t)stream;
+  HIP_OK(hipEventRecord(cx->ev0, st));
+  hipLaunchKernelGGL(k, grid, block, 0, st, cx->md, ds, dr, dt, C, nsweeps, sweep0,
+                     record_every, mask, seed, chain0, eval_only, ow, oh);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(cx->ev1, st));
+  cx->timed = true;
+  return 0;
+}
+
+int gst_sweep(void* ctx, const gst_state* state, const gst_records* rec, const gst_tape* tape,
+              int nchains, int nsweeps, long long sweep0, int record_every,
+              unsigned stage_mask, unsigned long long seed, long long chain0, void* stream) {
+  if (nsweeps < 0) return fail("gst_sweep: nsweeps < 0");
+  if (rec && record_every > 0 && rec->nrec < (nsweeps + record_every - 1) / record_every)
+    return fail("gst_sweep: record buffer too small");
+  return launch(static_cast<Ctx*>(ctx), state, rec, tape, nchains, nsweeps, sweep0,
+                record_every, stage_mask, seed, chain0, 0, nullptr, nullptr, stream);
+}
+
+int gst_eval_lnlike(void* ctx, const gst_state* state, int nchains, double* out_white,
+                    double* out_hyper, void* stream) {
+  if (!out_white || !out_hyper) return fail("gst_eval_lnlike: null outputs");
+  return launch(static_cast<Ctx*>(ctx), state, nullptr, nullptr, nchains, 0, 0, 0, 0u, 0ull,
+                0, 1, out_white, out_hyper, stream);
+}
+
+int gst_debug_stamps(void* ctx, unsigned long long* dev_buf) {
+  Ctx* cx = static_cast<Ctx*>(ctx);
+  if (!cx || !cx->has_model) return fail("gst_debug_stamps: no model");
+#ifdef GST_STAMPS
+  cx->md.stamps = dev_buf;
+  return 0;
+#else
+  (void)dev_buf;
+  return fail("gst_debug_stamps: library built without GST_STAMPS");
+#endif
+}
+
+int gst_sync(void* ctx, void* stream) {
+  Ctx* cx = static_cast<Ctx*>(ctx);
+  if (cx) HIP_OK(hipSetDevice(cx->device));
+  HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+  return 0;
+}
+
+int gst_last_sweep_ms(void* ctx, double* ms) {
+  Ctx* cx = static_cast<Ctx*>(ctx);
+  if (!cx || !ms) return fail("gst_last_sweep_ms: null argument");
+  if (!cx->timed) return fail("gst_last_sweep_ms: nothing launched");
+  HIP_OK(hipEventSynchronize(cx->ev1));
+  float f = 0.f;
+  HIP_OK(hipEventElapsedTime(&f, cx->ev0, cx->ev1));
+  *ms = f;
+  return 0;
+}
+
+}  // extern "C"

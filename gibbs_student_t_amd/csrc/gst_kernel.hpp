@@ -1,0 +1,959 @@
+// Persistent per-chain Gibbs sweep kernel for gfx950 (MI355X, CDNA4).
+//
+// One 64-lane wavefront owns one chain for a whole launch of `nsweeps` sweeps of the
+// reference sampler (/root/reference/gibbs.py, Gibbs.sample loop gibbs.py:354-380).
+// Chains are independent, so waves never synchronise with each other: there is no
+// __syncthreads, only in-order same-wave LDS traffic.
+//
+// Matrix layout ("8x8 cyclic"): lane = 8p + q owns elements (8r+p, 8s+q) of the symmetric
+// system matrix, r >= s, in registers L[SL(r,s)].  Internal column order is
+//     [ timing model (ntm) | pad to 8*K0 | Fourier (nf) | r (augmented row) | pad ]
+// so that (i) the timing-model block, whose prior never changes inside a sweep, is
+// eliminated once per sweep (its Schur complement S0 is kept in registers) and (ii) the
+// residual column rides along as an augmented row whose elimination yields L^-1 d, i.e.
+// d^T Sigma^-1 d, for free.  Every MH step of the red-noise hyper block only refactors the
+// (nf+1)-row Fourier block S0 + diag(phi^-1).
+//
+// Stages per sweep (gibbs.py stage order, semantically binding):
+//   white MH (20 steps)      gibbs.py:114-143, lnL gibbs.py:262-284
+//   Gram T^T N^-1 [T|r]       gibbs.py:302-304  -- fp64 MFMA 16x16x4, T shared by all chains
+//   hyper MH (10 steps)      gibbs.py:80-111,  lnL gibbs.py:288-329
+//   b draw (quirk :373)       gibbs.py:145-182  -- Cholesky draw mu + L^-T eta
+//   theta, z, alpha, nu       gibbs.py:185-259
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "philox.hpp"
+
+namespace gst {
+
+typedef double v4d __attribute__((ext_vector_type(4)));
+
+// waves (chains) per workgroup: as many as the per-wave LDS footprint allows (one
+// workgroup per CU at these sizes; never more than 4 = one wave per SIMD)
+__host__ __device__ constexpr int wpb_for(int MT, int NS) {
+  return (8 * MT * 8 + 16 * 17 + 64 * NS + 7 * 8 * MT + 32 + 128 +
+          64 * ((MT - 2) * (MT - 1) / 2)) * 8 * 4 <= 160 * 1024
+             ? 4
+             : 2;
+}
+constexpr int NWHITE = 20;
+constexpr int NHYPER = 10;
+
+struct DevModel {
+  const double* Tmf;     // [nks][NT][64]: MFMA-packed augmented T, internal column order
+  const double* Tcol;    // [m][npad]: T column-major, reference column order, zero padded
+  const double* resid;   // [npad]
+  const double* sig2;    // [npad]  toaerrs**2
+  const double* lfreq;   // [nf]    log(Ffreqs)
+  const double* ldf;     // [nf]    log(repeat(df, 2))
+  const double* dfA;     // [32]    n*(nu/2)*log(nu/2)
+  const double* dfB;     // [32]    n*gammaln(nu/2)
+  const int* ref2int;    // [m]     reference column -> internal index
+  int n, m, nf, ntm, ntm_pad, raug, nks, npad, nslot_toa;
+  int P;
+  int idx_efac, idx_equad, idx_logA, idx_gamma;
+  double efac_const;
+  double pmin[4], pmax[4], lp_in[4];
+  int hind[4], nh, wind[4], nw;
+  double sig_h, sig_w;
+  double mh_cdf[5], mh_size[5];
+  int model, vary_df, vary_alpha;
+  double mk, k1mm, pspin;
+  double tm_phiinv, logdet_phi_tm;
+  double log_fyr, log_12pi2;
+  unsigned long long* stamps;  // diagnostic build only (GST_STAMPS): [C][8] cycle sums
+};
+
+struct DevState {
+  double *x, *b, *z, *alpha, *pout, *theta, *nu;
+  int* status;
+};
+struct DevRec {
+  double *x, *b, *z, *alpha, *pout, *theta, *nu;
+  int nrec;
+};
+struct DevTape {
+  const double* data;
+  int stride;
+};
+
+// tape layout offsets (see gst.h)
+constexpr int TP_WHITE = 0, TP_HYPER = 80, TP_DELTA = 120;
+
+__host__ __device__ constexpr int SL(int r, int s) { return r * (r + 1) / 2 + s; }
+
+#ifdef GST_STAMPS
+#define GST_STAMP_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_t0 = 0;
+#define GST_STAMP_START st_t0 = __builtin_amdgcn_s_memtime();
+#define GST_STAMP(i)                                              \
+  {                                                               \
+    const unsigned long long t1_ = __builtin_amdgcn_s_memtime(); \
+    st_acc[i] += t1_ - st_t0;                                     \
+    st_t0 = t1_;                                                  \
+  }
+#define GST_STAMP_FLUSH                                             \
+  if (md.stamps && lane == 0)                                       \
+    for (int i_ = 0; i_ < 8; ++i_) md.stamps[(size_t)c * 8 + i_] += st_acc[i_];
+#else
+#define GST_STAMP_DECL
+#define GST_STAMP_START
+#define GST_STAMP(i)
+#define GST_STAMP_FLUSH
+#endif
+
+__device__ __forceinline__ double rdlane(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Cross-lane moves within a 16-lane row by DPP (VALU speed, no LDS traffic).
+template <int CTRL>
+__device__ __forceinline__ double dpp(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_ROR4 = 0x124, DPP_ROR8 = 0x128;
+
+// Sum over the wave: quad butterflies + row rotations give every lane its 16-lane row sum,
+// then the four row sums are combined in a fixed order from lanes 0/16/32/48, so the result
+// is bitwise identical (uniform) in every lane.
+__device__ __forceinline__ double wave_sum(double v) {
+  v += dpp<DPP_XOR1>(v);
+  v += dpp<DPP_XOR2>(v);
+  v += dpp<DPP_ROR4>(v);
+  v += dpp<DPP_ROR8>(v);
+  return (rdlane(v, 0) + rdlane(v, 16)) + (rdlane(v, 32) + rdlane(v, 48));
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+  v = fmax(v, dpp<DPP_XOR1>(v));
+  v = fmax(v, dpp<DPP_XOR2>(v));
+  v = fmax(v, dpp<DPP_ROR4>(v));
+  v = fmax(v, dpp<DPP_ROR8>(v));
+  return fmax(fmax(rdlane(v, 0), rdlane(v, 16)), fmax(rdlane(v, 32), rdlane(v, 48)));
+}
+
+// Sum over p (lane bits 3..5) of the lanes with q == qq (lane = 8p + q), uniform result.
+__device__ __forceinline__ double col_sum(double v, int qq) {
+  v += dpp<DPP_ROR8>(v);  // (l + 8) mod 16 == l ^ 8
+  return (rdlane(v, qq) + rdlane(v, qq + 16)) + (rdlane(v, qq + 32) + rdlane(v, qq + 48));
+}
+
+// 1/sqrt(a): hardware estimate + two Newton steps (full double accuracy to ~1 ulp).
+__device__ __forceinline__ double rsqrt_nr(double a) {
+  double y = __builtin_amdgcn_rsq(a);
+  y = y * fma(-0.5 * a * y, y, 1.5);
+  y = y * fma(-0.5 * a * y, y, 1.5);
+  return y;
+}
+
+__device__ __forceinline__ void lds_order() {
+  // Same-wave LDS accesses execute in issue order; this only stops the compiler from
+  // moving memory operations across the hand-off point.
+  __builtin_amdgcn_wave_barrier();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+__device__ __forceinline__ double pget(const double (&x)[4], int i) {
+  return i == 0 ? x[0] : (i == 1 ? x[1] : (i == 2 ? x[2] : x[3]));
+}
+__device__ __forceinline__ int iget4(const int (&a)[4], int i) {
+  return i == 0 ? a[0] : (i == 1 ? a[1] : (i == 2 ? a[2] : a[3]));
+}
+
+// x + (xi * sigma) * scale exactly as numpy evaluates it (gibbs.py:97,130): no FMA, so the
+// chain positions match the reference bit for bit.
+__device__ __forceinline__ double mh_jump(double x, double xi, double sig, double scale) {
+#pragma clang fp contract(off)
+  const double step = (xi * sig) * scale;
+  return x + step;
+}
+
+// numpy legacy binomial(1, p) given its uniform (inversion branch, random_binomial).
+__device__ __forceinline__ int bern_legacy(double p, double u) {
+  if (p == 0.0) return 0;
+  if (p <= 0.5) return u > exp(log(1.0 - p)) ? 1 : 0;
+  const double qq = 1.0 - p;
+  return u > exp(log(1.0 - qq)) ? 0 : 1;
+}
+
+// Box-Muller normal from one Philox draw.
+__device__ __forceinline__ double normal_from(const Rng& rng, uint32_t index, uint32_t tag) {
+  double a, b;
+  rng.uniform2(index, tag, a, b);
+  return sqrt(-2.0 * log(1.0 - a)) * cospi(2.0 * b);
+}
+
+// Marsaglia-Tsang Gamma(a, 1); a < 1 via the a+1 boost.  Bounded attempts.
+__device__ double gamma_mt(double a, const Rng& rng, uint32_t index, uint32_t tag) {
+  double boost = 1.0;
+  if (a < 1.0) {
+    double ub, unused;
+    rng.uniform2(index, tag | 0xFFFFFFu, ub, unused);
+    boost = pow(1.0 - ub, 1.0 / a);
+    a += 1.0;
+  }
+  const double d = a - 1.0 / 3.0;
+  const double cc = 1.0 / sqrt(9.0 * d);
+#pragma unroll 1
+  for (uint32_t att = 0; att < 256u; ++att) {
+    double u1, u2, u3, u4;
+    rng.uniform2(index, tag | (2u * att), u1, u2);
+    rng.uniform2(index, tag | (2u * att + 1u), u3, u4);
+    const double xn = sqrt(-2.0 * log(1.0 - u1)) * cospi(2.0 * u2);
+    double v = 1.0 + cc * xn;
+    if (v <= 0.0) continue;
+    v = v * v * v;
+    const double x2 = xn * xn;
+    if (u3 < 1.0 - 0.0331 * x2 * x2) return d * v * boost;
+    if (log(u3) < 0.5 * x2 + d * (1.0 - v + log(v))) return d * v * boost;
+  }
+  return d * boost;
+}
+
+// Right-looking LDL^T-scaled Cholesky on the cyclic register layout.
+//
+// Registers keep RAW columns: after column k is eliminated, slot values hold
+// a_ik = L_ik * sqrt(a_kk) (the a_kk are the pivots), so L_ik = a_ik / sqrt(a_kk) is never
+// formed inside the factorisation; the rank-1 update is a_ij -= (a_ik / a_kk) * a_jk.
+// After each step every lane publishes its slot column that holds the next column into
+// its own LDS column buffer colq[q][.] (no owner test, no selects); step k reads the
+// buffer of q = k % 8.  Rows <= k are masked on the reading side (only slot K can hold
+// them).  The slot column holding column k+1 is updated first so its publication (the
+// step-to-step dependency through LDS) is issued before the rest of the trailing update.
+// Outputs per column: the pivot a_kk (apiv), the augmented-row entry a_{raug,k} (zraw),
+// sum log a_kk (= log|Sigma| over these columns, as mantissa product + exponent sum) and
+// sum zraw^2 / a_kk (= the d^T Sigma^-1 d contribution).
+struct CholCtx {
+  double* colq;   // [8][MP]
+  double* zraw;   // [MP]
+  double* apiv;   // [MP]
+  int lane, p, q, kend, raug;
+  double mant, quad;
+  int expo, fail;
+};
+
+template <int MT>
+__device__ __forceinline__ void chol_publish(const double (&L)[SL(MT, 0)], CholCtx& cc, int s) {
+  double* dst = cc.colq + 8 * MT * cc.q + cc.p;
+#pragma unroll
+  for (int r = 0; r < MT; ++r)
+    if (r >= s) dst[8 * r] = L[SL(r, s)];
+}
+
+template <int MT, int K, int S1>
+__device__ __forceinline__ void chol_step(double (&L)[SL(MT, 0)], CholCtx& cc, int kk) {
+  // column k = 8K + kk was published by lanes q == kk into colq[kk]
+  const int k = 8 * K + kk;
+  const double* col = cc.colq + 8 * MT * kk;
+  lds_order();
+  double lr[MT], lc[MT];
+#pragma unroll
+  for (int r = K; r < MT; ++r) {
+    lr[r] = col[8 * r + cc.p];
+    lc[r] = col[8 * r + cc.q];
+  }
+  const double akk = col[k];
+  const double zk = col[cc.raug];
+  lr[K] = (8 * K + cc.p > k) ? lr[K] : 0.0;
+  lc[K] = (8 * K + cc.q > k) ? lc[K] : 0.0;
+  cc.fail |= !(akk > 0.0) ? 1 : 0;
+  const double sk = 1.0 / akk;
+  int e;
+  const double mm = frexp(akk, &e);
+  cc.mant *= mm;
+  cc.expo += e;
+  cc.quad = fma(zk * zk, sk, cc.quad);
+  cc.apiv[k] = akk;
+  cc.zraw[k] = zk;
+#pragma unroll
+  for (int r = K; r < MT; ++r) lr[r] *= sk;
+  // slot column S1 (holds column k+1) first, then publish it
+  if constexpr (S1 < MT) {
+#pragma unroll
+    for (int r = S1; r < MT; ++r) L[SL(r, S1)] = fma(-lr[r], lc[S1], L[SL(r, S1)]);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    chol_publish<MT>(L, cc, S1);
+  }
+#pragma unroll
+  for (int s = K; s < MT; ++s) {
+    if (s == S1 || (S1 == K + 1 && s == K)) continue;  // slot column K is done when kk == 7
+#pragma unroll
+    for (int r = s; r < MT; ++r) L[SL(r, s)] = fma(-lr[r], lc[s], L[SL(r, s)]);
+  }
+}
+
+template <int MT, int K, int KHI>
+__device__ __forceinline__ void chol_panel(double (&L)[SL(MT, 0)], CholCtx& cc) {
+#pragma unroll 1
+  for (int kk = 0; kk < 7; ++kk) {
+    if (8 * K + kk >= cc.kend) return;
+    chol_step<MT, K, K>(L, cc, kk);
+  }
+  if (8 * K + 7 >= cc.kend) return;
+  chol_step<MT, K, K + 1>(L, cc, 7);
+  if constexpr (K + 1 < KHI) chol_panel<MT, K + 1, KHI>(L, cc);
+}
+
+// Eliminate columns [8*KLO, kend) (kend <= 8*KHI), updating the trailing slots.
+template <int MT, int KLO, int KHI>
+__device__ __forceinline__ void chol_range(double (&L)[SL(MT, 0)], CholCtx& cc) {
+  if (cc.kend <= 8 * KLO) return;
+  chol_publish<MT>(L, cc, KLO);
+  chol_panel<MT, KLO, KHI>(L, cc);
+  lds_order();
+}
+
+template <int MT, int NS, int K0, bool TAPE>
+__global__ void __launch_bounds__(64 * wpb_for(MT, NS))
+    gst_sweep_kernel(const DevModel md, const DevState st, const DevRec rec, const DevTape tape,
+                     int C, int nsweeps, long long sweep0, int record_every, unsigned mask,
+                     unsigned long long seed, long long chain0, int eval_only, double* out_w,
+                     double* out_h) {
+  constexpr int NSL = SL(MT, 0);
+  constexpr int NT = MT / 2;          // 16-wide MFMA tiles
+  constexpr int NTT = NT * (NT + 1) / 2;
+  constexpr int MP = 8 * MT;
+  constexpr int NS0 = SL(MT - K0, 0);  // S0 slots (r >= s >= K0)
+  constexpr int TB_LD = 17;
+  constexpr int WPB = wpb_for(MT, NS);
+  constexpr int LDSW = 8 * MP + 16 * TB_LD + 64 * NS + 7 * MP + 32 + 4 * 32;
+  __shared__ double smem[WPB][LDSW];
+  __shared__ double s0mem[WPB][NS0 * 64];   // Schur complement S0, [slot][lane]
+
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * WPB + wv;
+  if (c >= C) return;
+  const int p = lane >> 3, q = lane & 7;
+
+  double* colq = smem[wv];            // [8][MP] published columns
+  double* tbuf = colq + 8 * MP;       // 16 x TB_LD Gram tile transpose
+  double* vbuf = tbuf + 16 * TB_LD;   // per-TOA scratch (weights), 64*NS
+  double* bbuf = vbuf + 64 * NS;      // b, reference order
+  double* phbuf = bbuf + MP;          // phi^-1 by internal index
+  double* zraw = phbuf + MP;          // a_{raug,k}
+  double* apiv = zraw + MP;           // pivots a_kk
+  double* wvec = apiv + MP;           // back-substitution rhs
+  double* xbuf = wvec + MP;           // scratch (Delta, solution; internal order)
+  double* yinv = xbuf + MP;           // 1/sqrt(a_kk)
+  double* dfbuf = yinv + MP;          // 32
+  double* mhv = dfbuf + 32;           // [30][4] MH variates: u_scale, index, jump, log(u_acc)
+  double* S0 = s0mem[wv] + lane;      // S0[64 * slot]
+
+  const int n = md.n, m = md.m, P = md.P, raug = md.raug;
+  const int npad = md.npad;
+  const long long gch = chain0 + c;
+
+  Rng rng;
+  rng.k0 = (uint32_t)(seed & 0xffffffffull);
+  rng.k1 = (uint32_t)(seed >> 32);
+  rng.chain = (uint32_t)gch;
+  rng.sweep = 0;
+
+  // ---------------- load chain state ----------------
+  double xv[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (j < P) xv[j] = st.x[(size_t)c * P + j];
+  double theta = st.theta[c];
+  double nu = st.nu[c];
+  for (int j = lane; j < MP; j += 64) bbuf[j] = (j < m) ? st.b[(size_t)c * m + j] : 0.0;
+  for (int j = lane; j < MP; j += 64) phbuf[j] = 0.0;
+
+  double rr[NS], s2[NS], al[NS], po[NS], yv[NS];
+  unsigned zb = 0u, vmask = 0u;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int t = 64 * s + lane;
+    const bool ok = t < n;
+    vmask |= ok ? (1u << s) : 0u;
+    rr[s] = ok ? md.resid[t] : 0.0;
+    s2[s] = ok ? md.sig2[t] : 1.0;
+    al[s] = ok ? st.alpha[(size_t)c * n + t] : 1.0;
+    po[s] = ok ? st.pout[(size_t)c * n + t] : 0.0;
+    const double zz = ok ? st.z[(size_t)c * n + t] : 0.0;
+    zb |= (zz != 0.0) ? (1u << s) : 0u;
+    yv[s] = 0.0;
+  }
+  int status = 0;
+  lds_order();
+
+  auto compute_Tb = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (s < md.nslot_toa) {
+        double tb = 0.0;
+        const double* tc = md.Tcol + 64 * s + lane;
+#pragma unroll 4
+        for (int j = 0; j < m; ++j) tb = fma(tc[(size_t)j * npad], bbuf[j], tb);
+        yv[s] = rr[s] - tb;
+      } else {
+        yv[s] = 0.0;
+      }
+    }
+  };
+
+  auto lnprior = [&](const double (&xq)[4]) __attribute__((always_inline)) -> double {
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j < P) s += (xq[j] >= md.pmin[j] && xq[j] <= md.pmax[j]) ? md.lp_in[j] : -INFINITY;
+    return s;
+  };
+
+  auto efac2_of = [&](const double (&xq)[4]) __attribute__((always_inline)) -> double {
+    const double ef = md.idx_efac >= 0 ? pget(xq, md.idx_efac) : md.efac_const;
+    return ef * ef;
+  };
+
+  // white-noise conditional likelihood (gibbs.py:262-284)
+  auto lnl_white = [&](const double (&xq)[4]) __attribute__((always_inline)) -> double {
+    const double ef2 = efac2_of(xq);
+    const double Q = exp(2.0 * pget(xq, md.idx_equad) * 2.302585092994045684);
+    double sl = 0.0, sq = 0.0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (vmask & (1u << s)) {
+        const double N0 = ef2 * s2[s] + Q;
+        const double N = ((zb >> s) & 1u ? al[s] : 1.0) * N0;
+        sl += log(N);
+        sq += yv[s] * yv[s] / N;
+      }
+    }
+    sl = wave_sum(sl);
+    sq = wave_sum(sq);
+    return -0.5 * (sl + sq);
+  };
+
+  // MH variates of one sweep (30 steps: 20 white then 10 hyper), produced in parallel by
+  // lanes 0..29: u_scale, parameter index, jump normal, log(u_accept) (gibbs.py:95-104,
+  // 128-137).  Tape mode copies the reference's recorded values instead.
+  auto mh_variates = [&](const double* tp) __attribute__((always_inline)) {
+    if (lane < NWHITE + NHYPER) {
+      const bool white = lane < NWHITE;
+      const int step = white ? lane : lane - NWHITE;
+      double us, par, xi, la;
+      if (TAPE) {
+        const double* e = tp + (white ? TP_WHITE : TP_HYPER) + 4 * step;
+        us = e[0];
+        par = e[1];
+        xi = e[2];
+        la = log(e[3]);
+      } else {
+        const uint32_t tag = white ? TAG_WHITE : TAG_HYPER;
+        double ua, ub, uidx, unused;
+        rng.uniform2(0u, tag | (uint32_t)(3 * step), ua, ub);
+        us = ua;
+        la = log(ub);
+        xi = normal_from(rng, 0u, tag | (uint32_t)(3 * step + 1));
+        const int nind = white ? md.nw : md.nh;
+        rng.uniform2(0u, tag | (uint32_t)(3 * step + 2), uidx, unused);
+        int k = (int)(uidx * nind);
+        k = k < nind - 1 ? k : nind - 1;
+        par = (double)(white ? iget4(md.wind, k) : iget4(md.hind, k));
+      }
+      mhv[4 * lane + 0] = us;
+      mhv[4 * lane + 1] = par;
+      mhv[4 * lane + 2] = xi;
+      mhv[4 * lane + 3] = la;
+    }
+    lds_order();
+  };
+
+  // MH proposal of global step gs (gibbs.py:90-97 / 123-130); returns log(u_accept)
+  auto propose = [&](const double (&xq)[4], double (&qv)[4], int gs, double sig)
+      __attribute__((always_inline)) -> double {
+    const double us = mhv[4 * gs + 0];
+    const int par = (int)mhv[4 * gs + 1];
+    const double xi = mhv[4 * gs + 2];
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) cnt += (md.mh_cdf[i] <= us) ? 1 : 0;
+    cnt = cnt < 4 ? cnt : 4;
+    const double scale = md.mh_size[0] * (cnt == 0) + md.mh_size[1] * (cnt == 1) +
+                         md.mh_size[2] * (cnt == 2) + md.mh_size[3] * (cnt == 3) +
+                         md.mh_size[4] * (cnt == 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) qv[j] = (j == par) ? mh_jump(xq[j], xi, sig, scale) : xq[j];
+    return mhv[4 * gs + 3];
+  };
+
+  // ---------------- matrix state ----------------
+  double L[NSL];
+  double ld_tm_m = 1.0, quad_tm = 0.0, logdetN = 0.0, rNr = 0.0;
+  int ld_tm_e = 0, fail_tm = 0;
+
+  // Gram: G = T_aug^T diag(1/N) T_aug on fp64 MFMA, then TM elimination -> S0.
+  auto gram_and_tm = [&](const double (&xq)[4]) __attribute__((always_inline)) {
+    const double ef2 = efac2_of(xq);
+    const double Q = exp(2.0 * pget(xq, md.idx_equad) * 2.302585092994045684);
+    double sl = 0.0, sr = 0.0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int t = 64 * s + lane;
+      double w = 0.0;
+      if (vmask & (1u << s)) {
+        const double N = ((zb >> s) & 1u ? al[s] : 1.0) * (ef2 * s2[s] + Q);
+        sl += log(N);
+        sr += rr[s] * rr[s] / N;
+        w = 1.0 / N;
+      }
+      vbuf[t] = w;
+    }
+    logdetN = wave_sum(sl);
+    rNr = wave_sum(sr);
+    lds_order();
+    v4d acc[NTT];
+#pragma unroll
+    for (int i = 0; i < NTT; ++i) acc[i] = (v4d){0.0, 0.0, 0.0, 0.0};
+    const int tl = lane >> 4;
+    double tv[NT], tn[NT];
+#pragma unroll
+    for (int X = 0; X < NT; ++X) tv[X] = md.Tmf[X * 64 + lane];
+#pragma unroll 1
+    for (int ks = 0; ks < md.nks; ++ks) {
+      if (ks + 1 < md.nks) {
+        const double* src = md.Tmf + (size_t)(ks + 1) * NT * 64 + lane;
+#pragma unroll
+        for (int X = 0; X < NT; ++X) tn[X] = src[X * 64];
+      }
+      const double wt = vbuf[4 * ks + tl];
+#pragma unroll
+      for (int I = 0; I < NT; ++I) {
+        const double av = tv[I] * wt;
+#pragma unroll
+        for (int J = 0; J <= I; ++J) {
+          acc[I * (I + 1) / 2 + J] =
+              __builtin_amdgcn_mfma_f64_16x16x4f64(av, tv[J], acc[I * (I + 1) / 2 + J], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int X = 0; X < NT; ++X) tv[X] = tn[X];
+    }
+    // MFMA C layout (col = lane&15, row = lane>>4 + 4 reg) -> cyclic register layout
+#pragma unroll
+    for (int I = 0; I < NT; ++I) {
+#pragma unroll
+      for (int J = 0; J <= I; ++J) {
+        const v4d a = acc[I * (I + 1) / 2 + J];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) tbuf[(tl + 4 * g) * TB_LD + (lane & 15)] = a[g];
+        lds_order();
+#pragma unroll
+        for (int dr = 0; dr < 2; ++dr)
+#pragma unroll
+          for (int ds = 0; ds < 2; ++ds) {
+            const int r = 2 * I + dr, s = 2 * J + ds;
+            if (r >= s) L[SL(r, s)] = tbuf[(8 * dr + p) * TB_LD + 8 * ds + q];
+          }
+        lds_order();
+      }
+    }
+    // timing-model prior (1/tm_weight) on its diagonal; unit pivots on the pad columns
+#pragma unroll
+    for (int s = 0; s < K0; ++s) {
+      const int j = 8 * s + q;
+      if (p == q) L[SL(s, s)] = (j < md.ntm) ? L[SL(s, s)] + md.tm_phiinv : 1.0;
+    }
+    CholCtx cc{colq, zraw, apiv, lane, p, q, 8 * K0, raug, 1.0, 0.0, 0, 0};
+    chol_range<MT, 0, K0>(L, cc);
+    ld_tm_m = cc.mant;
+    ld_tm_e = cc.expo;
+    quad_tm = cc.quad;
+    fail_tm = cc.fail;
+#pragma unroll
+    for (int r = K0; r < MT; ++r)
+#pragma unroll
+      for (int s = K0; s <= r; ++s) S0[64 * SL(r - K0, s - K0)] = L[SL(r, s)];
+  };
+
+  // b-marginalised likelihood at xq (gibbs.py:288-329); factor left in L.
+  auto lnl_hyper = [&](const double (&xq)[4], int& failed) __attribute__((always_inline)) -> double {
+    const double lA = pget(xq, md.idx_logA);
+    const double g = pget(xq, md.idx_gamma);
+    // log phi_k = 2 lA ln10 - log(12 pi^2) + (g-3) log fyr - g log f_k + log df_k
+    const double lc = 2.0 * lA * 2.302585092994045684 - md.log_12pi2 + (g - 3.0) * md.log_fyr;
+    double lsum = 0.0;
+    for (int f = lane; f < md.nf; f += 64) {
+      const double lphi = lc - g * md.lfreq[f] + md.ldf[f];
+      lsum += lphi;
+      phbuf[md.ntm_pad + f] = exp(-lphi);
+    }
+    const double logdet_phi = wave_sum(lsum) + md.logdet_phi_tm;
+    lds_order();
+#pragma unroll
+    for (int r = K0; r < MT; ++r)
+#pragma unroll
+      for (int s = K0; s <= r; ++s) {
+        double v = S0[64 * SL(r - K0, s - K0)];
+        if (r == s && p == q) v += phbuf[8 * r + p];
+        L[SL(r, s)] = v;
+      }
+    CholCtx cc{colq, zraw, apiv, lane, p, q, raug, raug, 1.0, 0.0, 0, 0};
+    chol_range<MT, K0, MT>(L, cc);
+    const double mant = cc.mant, quad = cc.quad;
+    const int expo = cc.expo;
+    failed = cc.fail | fail_tm;
+    if (failed) return -INFINITY;
+    // log|Sigma| = sum log a_kk (pivots of the LDL^T-scaled elimination)
+    const double ld_sigma = log(ld_tm_m * mant) + (double)(ld_tm_e + expo) * 0.693147180559945309417;
+    double ll = -0.5 * (logdetN + rNr);
+    ll += 0.5 * ((quad_tm + quad) - ld_sigma - logdet_phi);
+    return ll;
+  };
+
+  const bool rec_on = record_every > 0 && !eval_only;
+  GST_STAMP_DECL
+  GST_STAMP_START
+  compute_Tb();
+  if (eval_only) nsweeps = 1;
+
+#pragma unroll 1
+  for (int it = 0; it < nsweeps; ++it) {
+    rng.sweep = (uint32_t)(sweep0 + it);
+    const double* tp = TAPE ? tape.data + ((size_t)c * nsweeps + it) * tape.stride : nullptr;
+
+    // ---- record the state at the start of the sweep (gibbs.py:355-361)
+    if (rec_on && (it % record_every) == 0) {
+      const int ri = it / record_every;
+      if (ri < rec.nrec) {
+        const size_t base = (size_t)c * rec.nrec + ri;
+        if (rec.x && lane < P) rec.x[base * P + lane] = pget(xv, lane);
+        if (rec.b)
+          for (int j = lane; j < m; j += 64) rec.b[base * m + j] = bbuf[j];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          const int t = 64 * s + lane;
+          if (vmask & (1u << s)) {
+            if (rec.z) rec.z[base * n + t] = (double)((zb >> s) & 1u);
+            if (rec.alpha) rec.alpha[base * n + t] = al[s];
+            if (rec.pout) rec.pout[base * n + t] = po[s];
+          }
+        }
+        if (lane == 0) {
+          if (rec.theta) rec.theta[base] = theta;
+          if (rec.nu) rec.nu[base] = nu;
+        }
+      }
+    }
+
+    const double x_last0 = pget(xv, P - 1);  // chain[ii, -1]
+    if (!eval_only) mh_variates(tp);
+    GST_STAMP(0)
+
+    // ---- white-noise MH block (gibbs.py:114-143); step -1 = the initial lnlike0
+    if ((mask & 1u) || eval_only) {
+      double l0 = 0.0, p0 = 0.0;
+#pragma unroll 1
+      for (int step = -1; step < NWHITE; ++step) {
+        double qv[4], luacc = 0.0;
+        if (step < 0) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) qv[j] = xv[j];
+        } else {
+          luacc = propose(xv, qv, step, md.sig_w);
+        }
+        const double p1 = lnprior(qv);
+        // out-of-prior: (l1 + -inf) - (l0 + p0) is -inf or NaN, never > log(u): skip lnL
+        if (step >= 0 && p1 == -INFINITY) continue;
+        const double l1 = lnl_white(qv);
+        if (step < 0) {
+          l0 = l1;
+          p0 = p1;
+          if (eval_only) {
+            if (lane == 0) out_w[c] = l1;
+            break;
+          }
+          continue;
+        }
+        if ((l1 + p1) - (l0 + p0) > luacc) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) xv[j] = qv[j];
+          l0 = l1;
+          p0 = p1;
+        }
+      }
+    }
+
+    GST_STAMP(1)
+    // ---- Gram + red-noise hyper MH block (gibbs.py:80-111, 288-329) + b draw (145-182)
+    // step -1: initial lnlike0; steps 0..9: proposals; step NHYPER: refactor at the final
+    // x for the b draw when the factor left in registers belongs to a rejected proposal.
+    bool redraw = false;
+    int fb = 0;
+    if ((mask & 6u) || eval_only) {
+      gram_and_tm(xv);
+      if (fail_tm) status |= 1;
+      GST_STAMP(2)
+      bool Lvalid = false;
+      double l0 = 0.0, p0 = 0.0;
+      const int first = ((mask & 2u) || eval_only) ? -1 : NHYPER;
+#pragma unroll 1
+      for (int step = first; step <= NHYPER; ++step) {
+        double qv[4], luacc = 0.0;
+        if (step == NHYPER) {
+          if (eval_only || !(mask & 4u)) break;
+          redraw = true;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (j < P) redraw = redraw && (xv[j] != x_last0);   // gibbs.py:373
+          if (mask & 128u) redraw = true;                        // direct update_b call
+          if (!redraw || Lvalid) break;
+        }
+        if (step < 0 || step == NHYPER) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) qv[j] = xv[j];
+        } else {
+          luacc = propose(xv, qv, NWHITE + step, md.sig_h);
+        }
+        const double p1 = lnprior(qv);
+        if (step >= 0 && step < NHYPER && p1 == -INFINITY) continue;
+        int f1 = 0;
+        const double l1 = lnl_hyper(qv, f1);
+        if (step == NHYPER) {
+          fb = f1;
+          break;
+        }
+        if (f1) status |= 1;
+        if (step < 0) {
+          l0 = l1;
+          p0 = p1;
+          Lvalid = true;
+          if (eval_only) {
+            if (lane == 0) out_h[c] = l1;
+            break;
+          }
+          continue;
+        }
+        if ((l1 + p1) - (l0 + p0) > luacc) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) xv[j] = qv[j];
+          l0 = l1;
+          p0 = p1;
+          Lvalid = true;
+        } else {
+          Lvalid = false;
+        }
+      }
+    }
+    if (eval_only) return;
+    GST_STAMP(3)
+
+    if (redraw) {
+      if (fb) {
+        status |= 2;
+      } else {
+        // y_k = 1/sqrt(a_kk); z = L^-1 d has z_k = zraw_k * y_k; L_ik = a_ik * y_k
+        for (int j = lane; j < raug; j += 64) yinv[j] = rsqrt_nr(apiv[j]);
+        lds_order();
+        // rhs w = z + eta
+        if (TAPE) {
+          // eta = L^T Delta, so that L^-T eta equals the reference's U S^-1/2 xi
+          for (int j = lane; j < MP; j += 64) xbuf[j] = 0.0;
+          lds_order();
+          for (int j = lane; j < m; j += 64) xbuf[md.ref2int[j]] = tp[TP_DELTA + j];
+          lds_order();
+#pragma unroll
+          for (int s = 0; s < MT; ++s) {
+            double part = 0.0;
+            const int j = 8 * s + q;
+#pragma unroll
+            for (int r = s; r < MT; ++r) {
+              const int i = 8 * r + p;
+              part += (i >= j && i < raug) ? L[SL(r, s)] * xbuf[i] : 0.0;
+            }
+            part += __shfl_xor(part, 8, 64);
+            part += __shfl_xor(part, 16, 64);
+            part += __shfl_xor(part, 32, 64);
+            if (p == 0 && j < raug) wvec[j] = (zraw[j] + part) * yinv[j];
+          }
+        } else {
+          for (int j = lane; j < raug; j += 64)
+            wvec[j] = zraw[j] * yinv[j] + normal_from(rng, (uint32_t)j, TAG_BDRAW);
+        }
+        lds_order();
+        // back substitution L^T v = w, descending columns:
+        // v_k = (w_k - y_k * sum_{i>k} a_ik v_i) * y_k
+        double vr[MT];
+#pragma unroll
+        for (int r = 0; r < MT; ++r) vr[r] = 0.0;
+#pragma unroll
+        for (int K = MT - 1; K >= 0; --K) {
+#pragma unroll 1
+          for (int kk = 7; kk >= 0; --kk) {
+            const int k = 8 * K + kk;
+            if (k >= raug) continue;
+            double part = 0.0;
+#pragma unroll
+            for (int r = K; r < MT; ++r) part = fma(L[SL(r, K)], vr[r], part);
+            const double sk = col_sum(part, kk);
+            const double yk = yinv[k];
+            const double vk = (wvec[k] - yk * sk) * yk;
+            vr[K] = (p == kk) ? vk : vr[K];
+            xbuf[k] = vk;
+          }
+        }
+        lds_order();
+        for (int j = lane; j < m; j += 64) bbuf[j] = xbuf[md.ref2int[j]];
+        lds_order();
+        compute_Tb();
+      }
+    }
+
+    GST_STAMP(4)
+    // ---- outlier block: theta (gibbs.py:185-198)
+    const double ef2 = efac2_of(xv);
+    const double Q = exp(2.0 * pget(xv, md.idx_equad) * 2.302585092994045684);
+    const bool mix = (md.model == 2) || (md.model == 3);
+    if ((mask & 8u) && mix) {
+      int zs = 0;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) zs += __popcll(__ballot(((zb & vmask) >> s) & 1u));
+      const double a = (double)zs + md.mk;
+      const double b = ((double)n - (double)zs) + md.k1mm;
+      if (TAPE) {
+        theta = tp[TP_DELTA + m];
+      } else {
+        const double ga = gamma_mt(a, rng, 0u, TAG_THETA);
+        const double gb = gamma_mt(b, rng, 1u, TAG_THETA);
+        theta = ga / (ga + gb);
+      }
+    }
+    // ---- z (gibbs.py:201-226)
+    if ((mask & 16u) && mix) {
+      const double SQ2PI = 2.5066282746310002;  // np.sqrt(2*np.pi)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        if (vmask & (1u << s)) {
+          const int t = 64 * s + lane;
+          const double N0 = ef2 * s2[s] + Q;
+          const double Nv = al[s] * N0;
+          const double y = yv[s];
+          const double sd1 = sqrt(Nv);
+          const double x1 = y / sd1;
+          double top = theta * (exp(-(x1 * x1) / 2.0) / SQ2PI / sd1);
+          if (md.model == 3) top = theta / md.pspin;
+          const double sd0 = sqrt(N0);
+          const double x0 = y / sd0;
+          const double bot = top + (1.0 - theta) * (exp(-(x0 * x0) / 2.0) / SQ2PI / sd0);
+          double qz = top / bot;
+          if (isnan(qz)) qz = 1.0;
+          po[s] = qz;
+          const double pz = qz < 1.0 ? qz : 1.0;
+          double u;
+          if (TAPE) {
+            u = tp[TP_DELTA + m + 1 + t];
+          } else {
+            double unused;
+            rng.uniform2((uint32_t)t, TAG_Z, u, unused);
+          }
+          const int zz = bern_legacy(pz, u);
+          zb = (zb & ~(1u << s)) | ((unsigned)zz << s);
+        }
+      }
+    }
+    // ---- alpha (gibbs.py:229-242)
+    if ((mask & 32u) && md.vary_alpha) {
+      int zs = 0;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) zs += __popcll(__ballot(((zb & vmask) >> s) & 1u));
+      if (zs >= 1) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          if (vmask & (1u << s)) {
+            const int t = 64 * s + lane;
+            const double zf = (double)((zb >> s) & 1u);
+            const double N0 = ef2 * s2[s] + Q;
+            const double top = ((yv[s] * yv[s]) * zf / N0 + nu) / 2.0;
+            double G;
+            if (TAPE) {
+              G = tp[TP_DELTA + m + 1 + n + t];
+            } else {
+              G = gamma_mt((zf + nu) / 2.0, rng, (uint32_t)t, TAG_ALPHA);
+            }
+            al[s] = top / G;
+          }
+        }
+      }
+    }
+    GST_STAMP(5)
+    // ---- nu (gibbs.py:244-259, 331-335)
+    if ((mask & 64u) && md.vary_df) {
+      double sa = 0.0;
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+        if (vmask & (1u << s)) sa += log(al[s]) + 1.0 / al[s];
+      const double S = wave_sum(sa);
+      double ll = -INFINITY;
+      if (lane < 30) {
+        const double h = (double)(lane + 1) / 2.0;
+        ll = -h * S + md.dfA[lane] - md.dfB[lane];
+      }
+      const double mx = wave_max(ll);
+      if (lane < 30) dfbuf[lane] = exp(ll - mx);
+      lds_order();
+      double u;
+      if (TAPE) {
+        u = tp[TP_DELTA + m + 1 + 2 * n];
+      } else {
+        double unused;
+        rng.uniform2(0u, TAG_DF, u, unused);
+      }
+      // numpy pairwise sum of 30 (8 accumulators), normalise, sequential cumsum, choice
+      double acc8[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc8[j] = dfbuf[j];
+#pragma unroll
+      for (int i = 8; i < 24; i += 8)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc8[j] += dfbuf[i + j];
+      double tot = ((acc8[0] + acc8[1]) + (acc8[2] + acc8[3])) +
+                   ((acc8[4] + acc8[5]) + (acc8[6] + acc8[7]));
+#pragma unroll
+      for (int i = 24; i < 30; ++i) tot += dfbuf[i];
+      double cdf[30];
+      double cs = 0.0;
+#pragma unroll
+      for (int i = 0; i < 30; ++i) {
+        cs += dfbuf[i] / tot;
+        cdf[i] = cs;
+      }
+      int cnt = 0;
+#pragma unroll
+      for (int i = 0; i < 30; ++i) cnt += (cdf[i] / cdf[29] <= u) ? 1 : 0;
+      cnt = cnt < 29 ? cnt : 29;
+      nu = (double)(cnt + 1);
+      lds_order();
+    }
+  }
+
+  GST_STAMP(6)
+  GST_STAMP_FLUSH
+  // ---------------- write back ----------------
+  if (lane < P) st.x[(size_t)c * P + lane] = pget(xv, lane);
+  for (int j = lane; j < m; j += 64) st.b[(size_t)c * m + j] = bbuf[j];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int t = 64 * s + lane;
+    if (vmask & (1u << s)) {
+      st.z[(size_t)c * n + t] = (double)((zb >> s) & 1u);
+      st.alpha[(size_t)c * n + t] = al[s];
+      st.pout[(size_t)c * n + t] = po[s];
+    }
+  }
+  if (lane == 0) {
+    st.theta[c] = theta;
+    st.nu[c] = nu;
+    if (st.status) st.status[c] |= status;
+  }
+}
+
+}  // namespace gst

@@ -1,0 +1,220 @@
+"""Device-side chain state and launches over the C ABI (libgst.so).
+
+PyTorch-ROCm owns every chain buffer (``torch.empty(..., device='cuda')``); the library
+receives raw ``data_ptr()`` values and the current HIP stream.  Nothing here computes a
+sweep on the CPU: a missing library or device raises.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+
+import numpy as np
+
+from . import _abi
+from .model import df_tables, hyper_white_indices
+
+MODEL_CODES = {"gaussian": _abi.GST_MODEL_GAUSSIAN, "t": _abi.GST_MODEL_T,
+               "mixture": _abi.GST_MODEL_MIXTURE, "vvh17": _abi.GST_MODEL_VVH17}
+STATE_KEYS = ("x", "b", "z", "alpha", "pout", "theta", "nu")
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def model_desc(pta, cfg: dict):
+    """Build the gst_model_desc for a ``model.PTA`` and Gibbs kwargs (gibbs.py:9-11).
+
+    Returns ``(desc, keepalive)``; keep ``keepalive`` referenced while ``desc`` is used.
+    """
+    names = [p.name for p in pta.params]
+    P = len(names)
+    hind, wind = hyper_white_indices(names)
+
+    def role(suffix):
+        for i, nm in enumerate(names):
+            if nm.endswith("_" + suffix):
+                return i
+        return -1
+
+    r = np.ascontiguousarray(pta.get_residuals()[0], dtype=np.float64)
+    T = np.ascontiguousarray(pta.get_basis()[0], dtype=np.float64)
+    n, m = T.shape
+    A, B = df_tables(n)
+    keep = {
+        "T": T, "r": r,
+        "err": np.ascontiguousarray(pta._toaerrs, dtype=np.float64),
+        "ff": np.ascontiguousarray(pta.Ffreqs, dtype=np.float64),
+        "pmin": np.array([p.pmin for p in pta.params], dtype=np.float64),
+        "pmax": np.array([p.pmax for p in pta.params], dtype=np.float64),
+        "hind": np.ascontiguousarray(hind, dtype=np.int32),
+        "wind": np.ascontiguousarray(wind, dtype=np.int32),
+        "A": np.ascontiguousarray(A, dtype=np.float64),
+        "B": np.ascontiguousarray(B, dtype=np.float64),
+    }
+    dp = lambda a: a.ctypes.data_as(_abi._D)  # noqa: E731
+    ip = lambda a: a.ctypes.data_as(_abi._I)  # noqa: E731
+    model = cfg.get("model", "gaussian")
+    if model not in MODEL_CODES:
+        raise ValueError(f"unknown model {model!r}")
+    if model == "vvh17" and cfg.get("pspin") is None:
+        raise ValueError("model='vvh17' needs pspin")
+    desc = _abi.ModelDesc(
+        n=n, m=m, nfourier=pta.nfourier, ntm=pta.ntm, nparams=P,
+        T=dp(keep["T"]), residuals=dp(keep["r"]), toaerrs=dp(keep["err"]),
+        ffreqs=dp(keep["ff"]), tm_weight=float(pta.tm_weight),
+        idx_efac=role("efac"), idx_equad=role("log10_equad"), idx_log10_A=role("log10_A"),
+        idx_gamma=role("gamma"),
+        efac_const=float(pta.efac_const if pta.efac_const is not None else 1.0),
+        pmin=dp(keep["pmin"]), pmax=dp(keep["pmax"]),
+        hyper_idx=ip(keep["hind"]), n_hyper=len(hind),
+        white_idx=ip(keep["wind"]), n_white=len(wind),
+        model=MODEL_CODES[model], vary_df=int(bool(cfg.get("vary_df", True))),
+        vary_alpha=int(bool(cfg.get("vary_alpha", True))),
+        theta_prior_beta=int(cfg.get("theta_prior", "beta") == "beta"),
+        mprior=float(cfg.get("m", 0.01)),
+        pspin=float(cfg.get("pspin") or 0.0),
+        df_A=dp(keep["A"]), df_B=dp(keep["B"]),
+    )
+    return desc, keep
+
+
+class NativeSampler:
+    """One HIP context + model + a batch of C chains resident on one GPU."""
+
+    def __init__(self, pta, cfg: dict, device: int = 0):
+        torch = _torch()
+        self.lib = _abi.load()
+        if not torch.cuda.is_available():
+            raise _abi.GstNativeError("no HIP device visible: the sampler runs only on GPU")
+        self.device = int(device)
+        self.tdev = torch.device("cuda", self.device)
+        ctx = ct.c_void_p()
+        _abi.check(self.lib, self.lib.gst_ctx_create(self.device, ct.byref(ctx)),
+                   "gst_ctx_create")
+        self.ctx = ctx
+        self.pta = pta
+        self.cfg = dict(cfg)
+        desc, keep = model_desc(pta, cfg)
+        _abi.check(self.lib, self.lib.gst_model_set(self.ctx, ct.byref(desc)), "gst_model_set")
+        self.n, self.m = pta.T.shape
+        self.P = len(pta.params)
+        self.stride = int(self.lib.gst_tape_stride(self.n, self.m))
+        self.C = 0
+        self.state = None
+
+    # ---- state ---------------------------------------------------------------------
+    def alloc(self, C: int):
+        torch = _torch()
+        f64 = dict(dtype=torch.float64, device=self.tdev)
+        self.C = int(C)
+        self.state = {
+            "x": torch.zeros((C, self.P), **f64), "b": torch.zeros((C, self.m), **f64),
+            "z": torch.zeros((C, self.n), **f64), "alpha": torch.ones((C, self.n), **f64),
+            "pout": torch.zeros((C, self.n), **f64), "theta": torch.zeros(C, **f64),
+            "nu": torch.zeros(C, **f64),
+            "status": torch.zeros(C, dtype=torch.int32, device=self.tdev),
+        }
+        return self.state
+
+    def set_state(self, **arrays):
+        torch = _torch()
+        for k, v in arrays.items():
+            if v is None:
+                continue
+            t = self.state[k]
+            src = torch.as_tensor(np.asarray(v, dtype=np.float64)).reshape(t.shape)
+            t.copy_(src.to(self.tdev))
+
+    def get_state(self):
+        return {k: v.detach().cpu().numpy().copy() for k, v in self.state.items()}
+
+    def _state_struct(self):
+        s = self.state
+        return _abi.State(*(ct.c_void_p(s[k].data_ptr()) for k in STATE_KEYS),
+                          ct.c_void_p(s["status"].data_ptr()))
+
+    def alloc_records(self, nrec: int, keys=STATE_KEYS):
+        torch = _torch()
+        f64 = dict(dtype=torch.float64, device=self.tdev)
+        shapes = {"x": (self.P,), "b": (self.m,), "z": (self.n,), "alpha": (self.n,),
+                  "pout": (self.n,), "theta": (), "nu": ()}
+        return {k: torch.empty((self.C, nrec) + shapes[k], **f64) for k in keys}
+
+    # ---- launches ------------------------------------------------------------------
+    def stream_ptr(self):
+        torch = _torch()
+        return ct.c_void_p(torch.cuda.current_stream(self.tdev).cuda_stream)
+
+    def sweep(self, nsweeps: int, *, records=None, record_every: int = 1,
+              mask: int = _abi.STAGE_ALL, seed: int = 0, sweep0: int = 0, chain0: int = 0,
+              tape=None):
+        """Launch ``nsweeps`` sweeps of all C chains.  ``records`` is a dict from
+        ``alloc_records`` (or None); ``tape`` a device float64 tensor [C, nsweeps, stride]."""
+        st = self._state_struct()
+        rec = None
+        if records is not None:
+            nrec = next(iter(records.values())).shape[1]
+            ptr = lambda k: ct.c_void_p(records[k].data_ptr()) if k in records else None  # noqa
+            rec = _abi.Records(*(ptr(k) for k in STATE_KEYS), nrec)
+        tp = None
+        if tape is not None:
+            if tuple(tape.shape) != (self.C, nsweeps, self.stride):
+                raise ValueError(f"tape shape {tuple(tape.shape)} != "
+                                 f"{(self.C, nsweeps, self.stride)}")
+            tp = _abi.Tape(ct.c_void_p(tape.data_ptr()), self.stride)
+        rc = self.lib.gst_sweep(self.ctx, ct.byref(st), ct.byref(rec) if rec else None,
+                                ct.byref(tp) if tp else None, self.C, int(nsweeps),
+                                int(sweep0), int(record_every if rec else 0), int(mask),
+                                int(seed) & 0xFFFFFFFFFFFFFFFF, int(chain0), self.stream_ptr())
+        _abi.check(self.lib, rc, "gst_sweep")
+
+    def eval_lnlike(self):
+        torch = _torch()
+        ow = torch.empty(self.C, dtype=torch.float64, device=self.tdev)
+        oh = torch.empty(self.C, dtype=torch.float64, device=self.tdev)
+        st = self._state_struct()
+        rc = self.lib.gst_eval_lnlike(self.ctx, ct.byref(st), self.C,
+                                      ct.c_void_p(ow.data_ptr()), ct.c_void_p(oh.data_ptr()),
+                                      self.stream_ptr())
+        _abi.check(self.lib, rc, "gst_eval_lnlike")
+        return ow.cpu().numpy(), oh.cpu().numpy()
+
+    def synchronize(self):
+        _abi.check(self.lib, self.lib.gst_sync(self.ctx, self.stream_ptr()), "gst_sync")
+
+    def last_kernel_ms(self):
+        ms = ct.c_double()
+        _abi.check(self.lib, self.lib.gst_last_sweep_ms(self.ctx, ct.byref(ms)),
+                   "gst_last_sweep_ms")
+        return ms.value
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.gst_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def pack_tape(ref_tape: dict, sweeps, n: int, m: int, stride: int):
+    """Golden-fixture tape (tools/gen_golden.py fields) -> [len(sweeps), stride] rows."""
+    rows = np.zeros((len(sweeps), stride))
+    for k, i in enumerate(sweeps):
+        row = rows[k]
+        for stage, off, ns in (("white", _abi.TAPE_WHITE, 20), ("hyper", _abi.TAPE_HYPER, 10)):
+            e = np.stack([ref_tape[f"{stage}_u"][i], ref_tape[f"{stage}_idx"][i].astype(float),
+                          ref_tape[f"{stage}_xi"][i], ref_tape[f"{stage}_acc"][i]], axis=1)
+            row[off:off + 4 * ns] = e.reshape(-1)
+        o = _abi.TAPE_DELTA
+        row[o:o + m] = np.nan_to_num(ref_tape["b_delta"][i])
+        row[o + m] = ref_tape["beta"][i]
+        row[o + m + 1:o + m + 1 + n] = ref_tape["z_u"][i]
+        row[o + m + 1 + n:o + m + 1 + 2 * n] = ref_tape["gamma"][i]
+        row[o + m + 1 + 2 * n] = ref_tape["df_u"][i]
+    return rows

@@ -1,0 +1,233 @@
+"""Drop-in ``Gibbs`` sampler (reference: /root/reference/gibbs.py, class Gibbs, :8-385).
+
+Same constructor, same public methods and attributes; every sweep runs on the GPU through
+libgst.so.  Extra keyword-only options: ``nchains`` (independent chains batched on the GPU;
+chain arrays gain a leading chain axis when > 1), ``seed`` (Philox key), ``device``,
+``record_every`` (thin the chain arrays) and ``chunk`` (sweeps per kernel launch).
+
+Differences from the reference, all documented in DESIGN.md:
+* variates come from on-device Philox4x32-10 instead of numpy's MT19937 stream, so chains
+  are distributionally -- not bitwise -- equal to the reference's for the same seed;
+* the b draw uses the Cholesky square root (mean = cho_solve(Sigma, d), the reference's own
+  expression at gibbs.py:321-322) instead of the SVD one at gibbs.py:169-171.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+
+import numpy as np
+import scipy.special
+
+from . import _abi
+from .native import STATE_KEYS, NativeSampler
+
+
+class Gibbs:
+    def __init__(self, pta, model="gaussian", tdf=4, m=0.01, vary_df=True,
+                 theta_prior="beta", vary_alpha=True, alpha=1e10, pspin=None, *,
+                 nchains=1, seed=None, device=0, record_every=1, chunk=512, verbose=False):
+        # gibbs.py:13-51
+        self.pta = pta
+        self.mp = m
+        self.theta_prior = theta_prior
+        self.pspin = pspin
+        self.vary_df = vary_df
+        self.vary_alpha = vary_alpha
+        self._residuals = self.pta.get_residuals()[0]
+        self._lmodel = model
+        self.nchains = int(nchains)
+        self.record_every = int(record_every)
+        self.chunk = int(chunk)
+        self.verbose = verbose
+        self.seed = int.from_bytes(os.urandom(8), "little") if seed is None else int(seed)
+        self._sweep_counter = 0
+        C, n = self.nchains, len(self._residuals)
+        mcols = self.pta.get_basis()[0].shape[1]
+        self.TNT = None
+        self.d = None
+        self._b_all = np.zeros((C, mcols))
+        self._pout_all = np.zeros((C, n))
+        z0 = 1.0 if model in ("t", "mixture", "vvh17") else 0.0
+        self._z_all = np.full((C, n), z0)
+        self._alpha_all = np.full((C, n), alpha if not vary_alpha else 1.0)
+        self._theta_all = np.full(C, float(m))
+        self._tdf_all = np.full(C, float(tdf))
+        cfg = dict(model=model, tdf=tdf, m=m, vary_df=vary_df, theta_prior=theta_prior,
+                   vary_alpha=vary_alpha, alpha=alpha, pspin=pspin)
+        self._native = NativeSampler(pta, cfg, device)
+        self._native.alloc(C)
+
+    # ---- reference attribute names (chain 0 view when nchains == 1) -----------------
+    def _view(self, a):
+        return a[0] if self.nchains == 1 else a
+
+    @property
+    def _b(self):
+        return self._view(self._b_all)
+
+    @property
+    def _z(self):
+        return self._view(self._z_all)
+
+    @property
+    def _alpha(self):
+        return self._view(self._alpha_all)
+
+    @property
+    def _pout(self):
+        return self._view(self._pout_all)
+
+    @property
+    def _theta(self):
+        return self._theta_all[0] if self.nchains == 1 else self._theta_all
+
+    @property
+    def tdf(self):
+        return self._tdf_all[0] if self.nchains == 1 else self._tdf_all
+
+    # ---- parameter helpers (gibbs.py:53-77) ----------------------------------------------
+    @property
+    def params(self):
+        return list(self.pta.params)
+
+    def map_params(self, xs):
+        return {par.name: x for par, x in zip(self.params, xs)}
+
+    def get_hyper_param_indices(self):
+        return np.array([i for i, p in enumerate(self.params)
+                         if "ecorr" in p.name or "log10_A" in p.name or "gamma" in p.name])
+
+    def get_white_noise_indices(self):
+        return np.array([i for i, p in enumerate(self.params)
+                         if "efac" in p.name or "equad" in p.name])
+
+    # ---- likelihoods ----------------------------------------------------------------------
+    def get_lnprior(self, xs):
+        """gibbs.py:337-339."""
+        return sum(p.get_logpdf(x) for p, x in zip(self.params, xs))
+
+    def get_lnlikelihood_df(self, df):
+        """gibbs.py:331-335 (host: a 30-point scalar function)."""
+        n = len(self._residuals)
+        a = self._alpha_all[0]
+        return -(df / 2) * np.sum(np.log(a) + 1 / a) + n * (df / 2) * np.log(df / 2) \
+            - n * scipy.special.gammaln(df / 2)
+
+    def _xs_all(self, xs):
+        xs = np.asarray(xs, dtype=np.float64)
+        if xs.ndim == 1:
+            xs = np.broadcast_to(xs, (self.nchains, xs.shape[0]))
+        return np.ascontiguousarray(xs)
+
+    def _push(self, xs_all):
+        self._native.set_state(x=xs_all, b=self._b_all, z=self._z_all, alpha=self._alpha_all,
+                               pout=self._pout_all, theta=self._theta_all, nu=self._tdf_all)
+
+    def _pull(self):
+        s = self._native.get_state()
+        self._b_all, self._z_all, self._alpha_all = s["b"], s["z"], s["alpha"]
+        self._pout_all, self._theta_all, self._tdf_all = s["pout"], s["theta"], s["nu"]
+        self.status = s["status"]
+        return s["x"]
+
+    def _lnlikes(self, xs):
+        self._push(self._xs_all(xs))
+        w, h = self._native.eval_lnlike()
+        return (w[0], h[0]) if self.nchains == 1 else (w, h)
+
+    def get_lnlikelihood_white(self, xs):
+        """gibbs.py:262-284, evaluated on the GPU."""
+        return self._lnlikes(xs)[0]
+
+    def get_lnlikelihood(self, xs):
+        """gibbs.py:288-329, evaluated on the GPU (Gram + Cholesky)."""
+        return self._lnlikes(xs)[1]
+
+    # ---- single-stage updates (each one GPU launch with a stage mask) -----------------------
+    def _stage(self, xs, mask):
+        self._push(self._xs_all(xs))
+        self._native.sweep(1, mask=mask, seed=self.seed, sweep0=self._sweep_counter)
+        self._sweep_counter += 1
+        x = self._pull()
+        return x[0] if self.nchains == 1 else x
+
+    def update_white_params(self, xs):
+        return self._stage(xs, _abi.STAGE_WHITE)
+
+    def update_hyper_params(self, xs):
+        return self._stage(xs, _abi.STAGE_HYPER)
+
+    def update_b(self, xs):
+        # a direct call draws unconditionally (gibbs.py:145-182); the :373 test belongs to
+        # sample() only
+        self._push(self._xs_all(xs))
+        self._native.sweep(1, mask=_abi.STAGE_B | _abi.STAGE_B_FORCE, seed=self.seed,
+                           sweep0=self._sweep_counter)
+        self._sweep_counter += 1
+        self._pull()
+        return self._b
+
+    def update_theta(self, xs):
+        self._stage(xs, _abi.STAGE_THETA)
+        return self._theta
+
+    def update_z(self, xs):
+        self._stage(xs, _abi.STAGE_Z)
+        return self._z
+
+    def update_alpha(self, xs):
+        self._stage(xs, _abi.STAGE_ALPHA)
+        return self._alpha
+
+    def update_df(self, xs):
+        self._stage(xs, _abi.STAGE_DF)
+        return self.tdf
+
+    # ---- the sampler (gibbs.py:342-385) ----------------------------------------------------
+    def sample(self, xs, niter=10000):
+        C, P = self.nchains, len(self.params)
+        n, mcols = len(self._residuals), self._b_all.shape[1]
+        every = max(1, self.record_every)
+        nrec = (niter + every - 1) // every
+        lead = () if C == 1 else (C,)
+        self.chain = np.zeros(lead + (nrec, P))
+        self.bchain = np.zeros(lead + (nrec, mcols))
+        self.thetachain = np.zeros(lead + (nrec,))
+        self.zchain = np.zeros(lead + (nrec, n))
+        self.alphachain = np.zeros(lead + (nrec, n))
+        self.poutchain = np.zeros(lead + (nrec, n))
+        self.dfchain = np.zeros(lead + (nrec,))
+        outs = {"x": self.chain, "b": self.bchain, "theta": self.thetachain,
+                "z": self.zchain, "alpha": self.alphachain, "pout": self.poutchain,
+                "nu": self.dfchain}
+        self._push(self._xs_all(xs))
+        chunk = max(every, (self.chunk // every) * every)
+        tstart = time.time()
+        done, ri = 0, 0
+        while done < niter:
+            k = min(chunk, niter - done)
+            kr = (k + every - 1) // every
+            recs = self._native.alloc_records(kr)
+            self._native.sweep(k, records=recs, record_every=every, seed=self.seed,
+                               sweep0=self._sweep_counter)
+            self._sweep_counter += k
+            for key in STATE_KEYS:
+                host = recs[key].cpu().numpy()
+                if C == 1:
+                    outs[key][ri:ri + kr] = host[0]
+                else:
+                    outs[key][:, ri:ri + kr] = host
+            done += k
+            ri += kr
+            if self.verbose:
+                sys.stdout.write("\r")
+                sys.stdout.write("Finished %g percent in %g seconds." %
+                                 (done / niter * 100, time.time() - tstart))
+                sys.stdout.flush()
+        x = self._pull()
+        return x[0] if C == 1 else x
+
+    def close(self):
+        self._native.close()

@@ -1,0 +1,165 @@
+/*
+ * gst.h -- C ABI of the MI355X-native batched Gibbs sampler (libgst.so).
+ *
+ * Drop-in boundary for the reference's Python sampler `Gibbs` (/root/reference/gibbs.py).
+ * The reference has no FFI: its "interface" is the Python class.  These entry points are
+ * what a ctypes (or cgo/JNI) binding of that class binds; INTEGRATION.md shows the
+ * ctypes stub.  Each entry point names the reference code it replaces.
+ *
+ * Conventions
+ *  - every function returns int: 0 = ok, < 0 = error; gst_last_error() gives the message
+ *    (thread-local).  No C++ exception crosses the ABI.
+ *  - all chain buffers are DEVICE pointers owned by the caller (PyTorch-ROCm tensors'
+ *    data_ptr()), fp64, laid out chain-major (struct-of-arrays); the library owns only the
+ *    model constants it uploads in gst_model_set and its own scratch.
+ *  - `stream` is a hipStream_t (may be NULL = default stream).  No host synchronisation
+ *    happens inside gst_sweep; gst_sync() waits for the stream.
+ *  - one ctx per device; not re-entrant across threads.
+ */
+#ifndef GST_H_
+#define GST_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GST_ABI_VERSION 1
+
+/* Outlier model kind: Gibbs(model=...) (gibbs.py:9,32,187-226). */
+enum gst_outlier_model {
+  GST_MODEL_GAUSSIAN = 0,
+  GST_MODEL_T = 1,
+  GST_MODEL_MIXTURE = 2,
+  GST_MODEL_VVH17 = 3
+};
+
+/* Stage mask for gst_sweep (the per-sweep stage order of gibbs.py:363-380). */
+enum gst_stage {
+  GST_STAGE_WHITE = 1u << 0, /* update_white_params  gibbs.py:114-143 */
+  GST_STAGE_HYPER = 1u << 1, /* update_hyper_params  gibbs.py:80-111 */
+  GST_STAGE_B = 1u << 2,     /* update_b             gibbs.py:145-182 (+ quirk :373) */
+  GST_STAGE_THETA = 1u << 3, /* update_theta         gibbs.py:185-198 */
+  GST_STAGE_Z = 1u << 4,     /* update_z             gibbs.py:201-226 */
+  GST_STAGE_ALPHA = 1u << 5, /* update_alpha         gibbs.py:229-242 */
+  GST_STAGE_DF = 1u << 6,    /* update_df            gibbs.py:244-259 */
+  GST_STAGE_ALL = 0x7fu,
+  GST_STAGE_B_FORCE = 1u << 7 /* draw b regardless of the gibbs.py:373 test (direct call) */
+};
+
+/* Model + sampler configuration.  Host pointers; copied by gst_model_set.
+ * Replaces: the pta protocol calls (gibbs.py:29,35,154-158,209-210,268-269,297-301,339)
+ * and the Gibbs constructor options (gibbs.py:9-51). */
+typedef struct gst_model_desc {
+  int n;           /* TOAs */
+  int m;           /* basis columns = nfourier + ntm (reference order [Fourier | TM]) */
+  int nfourier;    /* 2 * components */
+  int ntm;         /* timing-model columns */
+  int nparams;     /* P <= 4, sorted by name as enterprise does */
+  const double* T;         /* n x m, row-major, reference column order */
+  const double* residuals; /* n, seconds */
+  const double* toaerrs;   /* n, seconds */
+  const double* ffreqs;    /* nfourier (= repeat(f, 2)) */
+  double tm_weight;        /* timing-model prior variance (1e40, run_sims.py:27-29) */
+  /* parameter roles: index into the P-vector or -1 */
+  int idx_efac, idx_equad, idx_log10_A, idx_gamma;
+  double efac_const;       /* used when idx_efac < 0 */
+  const double* pmin;      /* P uniform prior bounds */
+  const double* pmax;
+  const int* hyper_idx;    /* hyper parameter indices (gibbs.py:64-69) */
+  int n_hyper;
+  const int* white_idx;    /* white parameter indices (gibbs.py:72-77) */
+  int n_white;
+  /* outlier model (Gibbs kwargs) */
+  int model;               /* enum gst_outlier_model */
+  int vary_df;
+  int vary_alpha;
+  int theta_prior_beta;    /* theta_prior == 'beta' */
+  double mprior;           /* m (a-priori outlier probability) */
+  double pspin;            /* vvh17 only */
+  const double* df_A;      /* 30: n*(nu/2)*log(nu/2) for nu=1..30 (gibbs.py:333-334) */
+  const double* df_B;      /* 30: n*gammaln(nu/2) */
+} gst_model_desc;
+
+/* Per-chain state, device pointers, chain-major.  x[C*P], b[C*m], z/alpha/pout[C*n],
+ * theta/nu[C]; status[C] may be NULL (bit 0: Cholesky failure seen in the hyper block,
+ * bit 1: b-draw factorisation failed and b was kept). */
+typedef struct gst_state {
+  double* x;
+  double* b;
+  double* z;
+  double* alpha;
+  double* pout;
+  double* theta;
+  double* nu;
+  int* status;
+} gst_state;
+
+/* Chain records (Gibbs.sample's chain/bchain/zchain/... arrays, gibbs.py:344-361):
+ * device pointers shaped [C][nrec][...]; any pointer may be NULL to skip that array.
+ * Sweep i of a launch is stored at record (i / record_every) when i % record_every == 0,
+ * holding the state at the START of the sweep, as the reference does (gibbs.py:355-361). */
+typedef struct gst_records {
+  double* x;
+  double* b;
+  double* z;
+  double* alpha;
+  double* pout;
+  double* theta;
+  double* nu;
+  int nrec;
+} gst_records;
+
+/* Injected-variate tape (parity mode), device pointer [C][nsweeps][stride] fp64 with
+ * stride = gst_tape_stride(n, m).  Per chain-sweep layout:
+ *   [0,80)   white MH step s: u_scale, param index, jump normal, accept uniform
+ *   [80,120) hyper MH step s: same
+ *   [120,120+m)  b draw term Delta = U S^-1/2 xi in reference order
+ *   then: beta value; n binomial uniforms; n gamma values; dof-choice uniform. */
+typedef struct gst_tape {
+  const double* data;
+  int stride;
+} gst_tape;
+
+int gst_version(void);
+int gst_tape_stride(int n, int m);
+int gst_last_error(char* buf, size_t len);
+
+int gst_ctx_create(int device, void** ctx);
+int gst_ctx_destroy(void* ctx);
+
+/* Upload model constants (replaces the pta object, gibbs.py:29-35). */
+int gst_model_set(void* ctx, const gst_model_desc* desc);
+
+/* Run `nsweeps` Gibbs sweeps for chains [0, nchains) (Gibbs.sample's loop body,
+ * gibbs.py:354-380).  `tape` NULL or tape->data NULL -> on-device Philox4x32-10 variates
+ * keyed by (seed, chain0 + c), counters by (sweep0 + i, stage, index): results do not
+ * depend on how chains are sharded over launches or GPUs. */
+int gst_sweep(void* ctx, const gst_state* state, const gst_records* rec,
+              const gst_tape* tape, int nchains, int nsweeps, long long sweep0,
+              int record_every, unsigned stage_mask, unsigned long long seed,
+              long long chain0, void* stream);
+
+/* Evaluate the two likelihoods for K (state, x) pairs without sampling:
+ *   out_white[k] = get_lnlikelihood_white(x_k)  (gibbs.py:262-284)
+ *   out_hyper[k] = get_lnlikelihood(x_k)        (gibbs.py:288-329)
+ * using chain k's b, z, alpha from `state` (x from state->x). */
+int gst_eval_lnlike(void* ctx, const gst_state* state, int nchains, double* out_white,
+                    double* out_hyper, void* stream);
+
+int gst_sync(void* ctx, void* stream);
+
+/* Diagnostic builds (-DGST_STAMPS) only: per-chain per-stage s_memtime cycle sums are
+ * accumulated into dev_buf[C][8]; returns an error in production builds. */
+int gst_debug_stamps(void* ctx, unsigned long long* dev_buf);
+
+/* Kernel-level timing of the last gst_sweep on its stream (hipEvents), milliseconds. */
+int gst_last_sweep_ms(void* ctx, double* ms);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GST_H_ */

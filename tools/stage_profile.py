@@ -1,0 +1,49 @@
+"""Per-stage cycle breakdown of the sweep kernel (diagnostic libgst_stamps.so).
+
+Usage: GST_LIB=gibbs_student_t_amd/libgst_stamps.so python tools/stage_profile.py [C] [S]
+Stamps fence the overlaps of the real kernel: read the SHARES, not the absolute length.
+"""
+import ctypes as ct
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+from gibbs_student_t_amd import _abi, data  # noqa: E402
+from gibbs_student_t_amd.model import PTA  # noqa: E402
+from gibbs_student_t_amd.native import NativeSampler  # noqa: E402
+
+STAGES = ["record", "white MH", "Gram+TM elim", "hyper MH (11 chol)", "b draw",
+          "theta+z+alpha", "nu"]
+
+
+def main():
+    C = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+    S = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+    pta = PTA(data.j1713())
+    ns = NativeSampler(pta, dict(model="mixture", vary_df=True, theta_prior="beta"), 0)
+    ns.alloc(C)
+    rng = np.random.default_rng(0)
+    x0 = np.stack([[rng.uniform(1, 7), rng.uniform(-18, -12), rng.uniform(-10, -5)]
+                   for _ in range(C)])
+    ns.set_state(x=x0, z=np.ones((C, ns.n)), alpha=np.ones((C, ns.n)),
+                 theta=np.full(C, 0.01), nu=np.full(C, 4.0))
+    ns.sweep(20, seed=1)
+    buf = torch.zeros((C, 8), dtype=torch.int64, device=ns.tdev)
+    _abi.check(ns.lib, ns.lib.gst_debug_stamps(ns.ctx, ct.c_void_p(buf.data_ptr())),
+               "gst_debug_stamps")
+    ns.sweep(S, seed=1, sweep0=20)
+    ns.synchronize()
+    ms = ns.last_kernel_ms()
+    cyc = buf.cpu().numpy().astype(np.float64)[:, :7] / S
+    tot = cyc.sum(axis=1)
+    print(f"C={C} S={S} kernel {ms:.2f} ms = {ms / S * 1e3:.1f} us/sweep; "
+          f"stamped cycles/sweep/chain median {np.median(tot):.0f}")
+    for i, nm in enumerate(STAGES):
+        print(f"  {nm:22s} {np.median(cyc[:, i]):10.0f} cyc  {np.median(cyc[:, i] / tot) * 100:5.1f} %")
+
+
+if __name__ == "__main__":
+    main()
