@@ -59,19 +59,20 @@ typedef void (*kfn_t)(const gst::DevModel, const gst::DevState, const gst::DevRe
                       const gst::DevTape, int, int, long long, int, unsigned,
                       unsigned long long, long long, int, double*, double*);
 
-template <int MT, int NS, int K0, bool TAPE>
+template <int MT, int NS, int K0, int RA, bool TAPE>
 kfn_t kfn() {
-  return &gst::gst_sweep_kernel<MT, NS, K0, TAPE>;
+  return &gst::gst_sweep_kernel<MT, NS, K0, RA, TAPE>;
 }
 
-// Instantiated shapes: MT = padded matrix dim / 8, NS = TOA slots of 64, K0 = TM panels.
-kfn_t pick(int MT, int NS, int K0, bool tape) {
-#define GST_CASE(mt, ns, k0)                                             \
-  if (MT == mt && NS == ns && K0 == k0)                                  \
-    return tape ? kfn<mt, ns, k0, true>() : kfn<mt, ns, k0, false>();
-  GST_CASE(10, 3, 2)
-  GST_CASE(10, 4, 2)
-  GST_CASE(12, 4, 2)
+// Instantiated shapes: MT = padded matrix dim / 8, NS = TOA slots of 64, K0 = timing-model
+// panels of 8, RA = augmented-row index = 8*K0 + nfourier (the elimination length).
+kfn_t pick(int MT, int NS, int K0, int RA, bool tape) {
+#define GST_CASE(mt, ns, k0, ra)                                          \
+  if (MT == mt && NS == ns && K0 == k0 && RA == ra)                       \
+    return tape ? kfn<mt, ns, k0, ra, true>() : kfn<mt, ns, k0, ra, false>();
+  GST_CASE(10, 2, 2, 76)   // J1713-like, n <= 128 (no_outlier datasets)
+  GST_CASE(10, 3, 2, 76)   // J1713+0747: n = 130, 30 red-noise components, 14 TM columns
+  GST_CASE(10, 4, 2, 76)   // n <= 256
 #undef GST_CASE
   return nullptr;
 }
@@ -132,18 +133,15 @@ int gst_model_set(void* ctx, const gst_model_desc* d) {
   const int raug = ntm_pad + nf;
   const int mpad = round_up(raug + 1, 16);
   const int MT = mpad / 8, K0 = ntm_pad / 8;
-  const int NS = (n + 63) / 64 <= 3 ? 3 : 4;
+  const int NS = (n + 63) / 64 <= 2 ? 2 : ((n + 63) / 64 <= 3 ? 3 : 4);
   const int npad = 64 * ((n + 63) / 64);
   if (round_up(n, 4) > 64 * NS) return fail("gst_model_set: n too large for TOA slots");
-  int MTk = MT;
-  if (!pick(MTk, NS, K0, false)) {
-    if (MT <= 12 && pick(12, 4, K0, false)) {
-      return fail("gst_model_set: internal: unsupported padded shape");
-    }
-    char b[160];
+  if (!pick(MT, NS, K0, raug, false)) {
+    char b[200];
     std::snprintf(b, sizeof b,
-                  "gst_model_set: no kernel instance for MT=%d NS=%d K0=%d (n=%d m=%d)", MT,
-                  NS, K0, n, m);
+                  "gst_model_set: no kernel instance for MT=%d NS=%d K0=%d RA=%d (n=%d m=%d "
+                  "nfourier=%d ntm=%d); add a GST_CASE in gst.hip",
+                  MT, NS, K0, raug, n, m, nf, ntm);
     return fail(b);
   }
   free_model(cx);
@@ -282,7 +280,7 @@ static int launch(Ctx* cx, const gst_state* s, const gst_records* r, const gst_t
   if (C <= 0) return 0;
   HIP_OK(hipSetDevice(cx->device));
   const bool tape = tp && tp->data;
-  kfn_t k = pick(cx->MT, cx->NS, cx->K0, tape);
+  kfn_t k = pick(cx->MT, cx->NS, cx->K0, cx->md.raug, tape);
   if (!k) return fail("gst: no kernel instance");
   gst::DevState ds{s->x, s->b, s->z, s->alpha, s->pout, s->theta, s->nu, s->status};
   gst::DevRec dr{};

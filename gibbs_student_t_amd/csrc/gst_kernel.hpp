@@ -235,7 +235,7 @@ struct CholCtx {
   double* colq;   // [8][MP]
   double* zraw;   // [MP]
   double* apiv;   // [MP]
-  int lane, p, q, kend, raug;
+  int lane, p, q, raug;
   double mant, quad;
   int expo, fail;
 };
@@ -248,70 +248,95 @@ __device__ __forceinline__ void chol_publish(const double (&L)[SL(MT, 0)], CholC
     if (r >= s) dst[8 * r] = L[SL(r, s)];
 }
 
-template <int MT, int K, int S1>
-__device__ __forceinline__ void chol_step(double (&L)[SL(MT, 0)], CholCtx& cc, int kk) {
-  // column k = 8K + kk was published by lanes q == kk into colq[kk]
-  const int k = 8 * K + kk;
-  const double* col = cc.colq + 8 * MT * kk;
-  lds_order();
+// 1/a: hardware estimate + two Newton steps.
+__device__ __forceinline__ double rcp_nr(double a) {
+  double y = __builtin_amdgcn_rcp(a);
+  y = fma(y, fma(-a, y, 1.0), y);
+  y = fma(y, fma(-a, y, 1.0), y);
+  return y;
+}
+
+// Raw column k as seen by this lane: rows 8r+p (lr), rows 8r+q (lc), the augmented row
+// entry, the pivot and its reciprocal.
+template <int MT>
+struct ColView {
   double lr[MT], lc[MT];
+  double zk, akk, sk;
+};
+
+template <int MT, int K, int KK>
+__device__ __forceinline__ void chol_load(const CholCtx& cc, ColView<MT>& c) {
+  const double* col = cc.colq + 8 * MT * KK;
+  const double* cr = col + cc.p;
+  const double* cq = col + cc.q;
 #pragma unroll
   for (int r = K; r < MT; ++r) {
-    lr[r] = col[8 * r + cc.p];
-    lc[r] = col[8 * r + cc.q];
+    c.lr[r] = cr[8 * r];
+    c.lc[r] = cq[8 * r];
   }
-  const double akk = col[k];
-  const double zk = col[cc.raug];
-  lr[K] = (8 * K + cc.p > k) ? lr[K] : 0.0;
-  lc[K] = (8 * K + cc.q > k) ? lc[K] : 0.0;
-  cc.fail |= !(akk > 0.0) ? 1 : 0;
-  const double sk = 1.0 / akk;
+  c.zk = col[cc.raug];
+}
+
+// Step k = 8K + KK, software-pipelined: the slot column holding column k+1 is updated
+// and published first, column k+1's loads and pivot reciprocal are issued, and only then
+// does the rest of step k's trailing update run (covering their latency).
+template <int MT, int K, int KK, int KEND>
+__device__ __forceinline__ void chol_step(double (&L)[SL(MT, 0)], CholCtx& cc,
+                                          ColView<MT>& cur) {
+  constexpr int k = 8 * K + KK;
+  constexpr int K1 = (KK == 7) ? K + 1 : K;  // slot column of column k+1
+  constexpr int KK1 = (KK + 1) & 7;
+  constexpr bool NEXT = k + 1 < KEND;
+  cur.lr[K] = (8 * K + cc.p > k) ? cur.lr[K] : 0.0;
+  cur.lc[K] = (8 * K + cc.q > k) ? cur.lc[K] : 0.0;
+  cc.fail |= !(cur.akk > 0.0) ? 1 : 0;
   int e;
-  const double mm = frexp(akk, &e);
+  const double mm = frexp(cur.akk, &e);
   cc.mant *= mm;
   cc.expo += e;
-  cc.quad = fma(zk * zk, sk, cc.quad);
-  cc.apiv[k] = akk;
-  cc.zraw[k] = zk;
+  cc.quad = fma(cur.zk * cur.zk, cur.sk, cc.quad);
+  cc.apiv[k] = cur.akk;
+  cc.zraw[k] = cur.zk;
+  double lrs[MT];
 #pragma unroll
-  for (int r = K; r < MT; ++r) lr[r] *= sk;
-  // slot column S1 (holds column k+1) first, then publish it
-  if constexpr (S1 < MT) {
+  for (int r = K; r < MT; ++r) lrs[r] = cur.lr[r] * cur.sk;
+  ColView<MT> nxt;
+  if constexpr (K1 < MT) {
 #pragma unroll
-    for (int r = S1; r < MT; ++r) L[SL(r, S1)] = fma(-lr[r], lc[S1], L[SL(r, S1)]);
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    chol_publish<MT>(L, cc, S1);
+    for (int r = K1; r < MT; ++r) L[SL(r, K1)] = fma(-lrs[r], cur.lc[K1], L[SL(r, K1)]);
+    if constexpr (NEXT) {
+      chol_publish<MT>(L, cc, K1);
+      nxt.akk = rdlane(L[SL(K1, K1)], 9 * KK1);
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      chol_load<MT, K1, KK1>(cc, nxt);
+      nxt.sk = rcp_nr(nxt.akk);
+    }
   }
 #pragma unroll
   for (int s = K; s < MT; ++s) {
-    if (s == S1 || (S1 == K + 1 && s == K)) continue;  // slot column K is done when kk == 7
+    if (s == K1 || (KK == 7 && s == K)) continue;  // slot column K is done when KK == 7
 #pragma unroll
-    for (int r = s; r < MT; ++r) L[SL(r, s)] = fma(-lr[r], lc[s], L[SL(r, s)]);
+    for (int r = s; r < MT; ++r) L[SL(r, s)] = fma(-lrs[r], cur.lc[s], L[SL(r, s)]);
   }
+  if constexpr (NEXT) chol_step<MT, K1, KK1, KEND>(L, cc, nxt);
 }
 
-template <int MT, int K, int KHI>
-__device__ __forceinline__ void chol_panel(double (&L)[SL(MT, 0)], CholCtx& cc) {
-#pragma unroll 1
-  for (int kk = 0; kk < 7; ++kk) {
-    if (8 * K + kk >= cc.kend) return;
-    chol_step<MT, K, K>(L, cc, kk);
-  }
-  if (8 * K + 7 >= cc.kend) return;
-  chol_step<MT, K, K + 1>(L, cc, 7);
-  if constexpr (K + 1 < KHI) chol_panel<MT, K + 1, KHI>(L, cc);
-}
-
-// Eliminate columns [8*KLO, kend) (kend <= 8*KHI), updating the trailing slots.
-template <int MT, int KLO, int KHI>
+// Eliminate columns [8*KLO, KEND) (compile-time: no branch between steps), updating the
+// trailing slots.
+template <int MT, int KLO, int KEND>
 __device__ __forceinline__ void chol_range(double (&L)[SL(MT, 0)], CholCtx& cc) {
-  if (cc.kend <= 8 * KLO) return;
+  static_assert(KEND > 8 * KLO && KEND <= 8 * MT, "bad elimination range");
   chol_publish<MT>(L, cc, KLO);
-  chol_panel<MT, KLO, KHI>(L, cc);
+  ColView<MT> c;
+  c.akk = rdlane(L[SL(KLO, KLO)], 0);
+  lds_order();
+  chol_load<MT, KLO, 0>(cc, c);
+  c.sk = rcp_nr(c.akk);
+  chol_step<MT, KLO, 0, KEND>(L, cc, c);
   lds_order();
 }
 
-template <int MT, int NS, int K0, bool TAPE>
+template <int MT, int NS, int K0, int RA, bool TAPE>
 __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
     gst_sweep_kernel(const DevModel md, const DevState st, const DevRec rec, const DevTape tape,
                      int C, int nsweeps, long long sweep0, int record_every, unsigned mask,
@@ -348,7 +373,9 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
   double* mhv = dfbuf + 32;           // [30][4] MH variates: u_scale, index, jump, log(u_acc)
   double* S0 = s0mem[wv] + lane;      // S0[64 * slot]
 
-  const int n = md.n, m = md.m, P = md.P, raug = md.raug;
+  static_assert(RA >= 8 * K0 + 1 && RA < 8 * MT, "augmented row out of range");
+  const int n = md.n, m = md.m, P = md.P;
+  constexpr int raug = RA;
   const int npad = md.npad;
   const long long gch = chain0 + c;
 
@@ -563,8 +590,8 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
       const int j = 8 * s + q;
       if (p == q) L[SL(s, s)] = (j < md.ntm) ? L[SL(s, s)] + md.tm_phiinv : 1.0;
     }
-    CholCtx cc{colq, zraw, apiv, lane, p, q, 8 * K0, raug, 1.0, 0.0, 0, 0};
-    chol_range<MT, 0, K0>(L, cc);
+    CholCtx cc{colq, zraw, apiv, lane, p, q, raug, 1.0, 0.0, 0, 0};
+    chol_range<MT, 0, 8 * K0>(L, cc);
     ld_tm_m = cc.mant;
     ld_tm_e = cc.expo;
     quad_tm = cc.quad;
@@ -597,8 +624,8 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
         if (r == s && p == q) v += phbuf[8 * r + p];
         L[SL(r, s)] = v;
       }
-    CholCtx cc{colq, zraw, apiv, lane, p, q, raug, raug, 1.0, 0.0, 0, 0};
-    chol_range<MT, K0, MT>(L, cc);
+    CholCtx cc{colq, zraw, apiv, lane, p, q, raug, 1.0, 0.0, 0, 0};
+    chol_range<MT, K0, RA>(L, cc);
     const double mant = cc.mant, quad = cc.quad;
     const int expo = cc.expo;
     failed = cc.fail | fail_tm;
