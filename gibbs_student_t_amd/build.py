@@ -35,7 +35,10 @@ def build(force: bool = False, verbose: bool = True, stamps: bool = False) -> st
     out = STAMPS_LIB if stamps else LIB
     if not force and not stamps and up_to_date():
         return LIB
+    # -amdgpu-mfma-vgpr-form: keep the fp64 MFMA accumulators in VGPRs (gfx950's unified
+    # register file); without it hipcc copies all 15 Gram tiles VGPR<->AGPR every k-step.
     cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-mllvm", "-amdgpu-mfma-vgpr-form",
            "-I", os.path.join(ROOT, "include"), "-I", CSRC,
            os.path.join(CSRC, "gst.hip"), "-o", out + ".tmp"]
     if stamps:

@@ -182,6 +182,30 @@ int gst_model_set(void* ctx, const gst_model_desc* d) {
     const double prev = pair == 0 ? 0.0 : d->ffreqs[2 * (pair - 1)];
     ldf[k] = std::log(d->ffreqs[2 * pair] - prev);
   }
+  // noise classes: TOAs with bit-identical sigma share N0 in the white likelihood
+  std::vector<double> csig2;
+  std::vector<double> ccount;
+  std::vector<int> cidx(npad, -1);
+  for (int t = 0; t < n; ++t) {
+    const double v = d->toaerrs[t] * d->toaerrs[t];
+    int u = 0;
+    while (u < (int)csig2.size() && csig2[u] != v) ++u;
+    if (u == (int)csig2.size()) {
+      if (csig2.size() >= 8) break;
+      csig2.push_back(v);
+      ccount.push_back(0.0);
+    }
+    cidx[t] = u;
+    ccount[u] += 1.0;
+  }
+  int ncls = (int)csig2.size();
+  for (int t = 0; t < n; ++t)
+    if (cidx[t] < 0) ncls = 0;  // more than 8 distinct sigmas: per-TOA path
+  double slf = 0.0, sldf = 0.0;
+  for (int k = 0; k < nf; ++k) {
+    slf += lf[k];
+    sldf += ldf[k];
+  }
   std::vector<double> dfA(32, 0.0), dfB(32, 0.0);
   for (int k = 0; k < 30; ++k) {
     dfA[k] = d->df_A[k];
@@ -208,6 +232,17 @@ int gst_model_set(void* ctx, const gst_model_desc* d) {
   md.dfB = (const double*)ptr;
   if (upload(cx, ref2int.data(), ref2int.size() * sizeof(int), &ptr)) return -1;
   md.ref2int = (const int*)ptr;
+  md.ncls = ncls;
+  if (ncls > 0) {
+    if (upload(cx, cidx.data(), cidx.size() * sizeof(int), &ptr)) return -1;
+    md.cidx = (const int*)ptr;
+    if (upload(cx, csig2.data(), csig2.size() * 8, &ptr)) return -1;
+    md.csig2 = (const double*)ptr;
+    if (upload(cx, ccount.data(), ccount.size() * 8, &ptr)) return -1;
+    md.ccount = (const double*)ptr;
+  }
+  md.sum_lfreq = slf;
+  md.sum_ldf = sldf;
 
   md.n = n;
   md.m = m;

@@ -34,7 +34,7 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 // waves (chains) per workgroup: as many as the per-wave LDS footprint allows (one
 // workgroup per CU at these sizes; never more than 4 = one wave per SIMD)
 __host__ __device__ constexpr int wpb_for(int MT, int NS) {
-  return (8 * MT * 8 + 16 * 17 + 64 * NS + 7 * 8 * MT + 32 + 128 +
+  return (8 * (8 * MT + 2) + 16 * 17 + 64 * NS + 7 * 8 * MT + 32 + 128 +
           64 * ((MT - 2) * (MT - 1) / 2)) * 8 * 4 <= 160 * 1024
              ? 4
              : 2;
@@ -52,6 +52,10 @@ struct DevModel {
   const double* dfA;     // [32]    n*(nu/2)*log(nu/2)
   const double* dfB;     // [32]    n*gammaln(nu/2)
   const int* ref2int;    // [m]     reference column -> internal index
+  const int* cidx;       // [npad]  noise class of each TOA (TOAs with equal sigma), or null
+  const double* csig2;   // [ncls]  sigma^2 of each class
+  const double* ccount;  // [ncls]  TOAs per class
+  int ncls;              // 0 = per-TOA white likelihood; 1..8 = class path
   int n, m, nf, ntm, ntm_pad, raug, nks, npad, nslot_toa;
   int P;
   int idx_efac, idx_equad, idx_logA, idx_gamma;
@@ -63,6 +67,7 @@ struct DevModel {
   int model, vary_df, vary_alpha;
   double mk, k1mm, pspin;
   double tm_phiinv, logdet_phi_tm;
+  double sum_lfreq, sum_ldf;  // sum_k log f_k, sum_k log df_k (closed-form log|phi|)
   double log_fyr, log_12pi2;
   unsigned long long* stamps;  // diagnostic build only (GST_STAMPS): [C][8] cycle sums
 };
@@ -85,8 +90,21 @@ constexpr int TP_WHITE = 0, TP_HYPER = 80, TP_DELTA = 120;
 
 __host__ __device__ constexpr int SL(int r, int s) { return r * (r + 1) / 2 + s; }
 
+// Stride (doubles) of the per-q column buffers: 8*MT + 2, so that the 16-lane groups of a
+// publishing ds_write_b64 (banks (a/4) mod 32) hit 32 distinct banks (8*MT alone puts the
+// even-q and odd-q lanes 4-way on the same banks).
+__host__ __device__ constexpr int CQ(int MT) { return 8 * MT + 2; }
+
 #ifdef GST_STAMPS
-#define GST_STAMP_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_t0 = 0;
+#define GST_STAMP_DECL \
+  unsigned long long st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_t0 = 0, st_s0 = 0;
+#define GST_SUB_BEGIN st_s0 = __builtin_amdgcn_s_memtime();
+#define GST_SUB_END(i)                                            \
+  {                                                               \
+    const unsigned long long t1_ = __builtin_amdgcn_s_memtime(); \
+    st_acc[i] += t1_ - st_s0;                                     \
+    st_s0 = t1_;                                                  \
+  }
 #define GST_STAMP_START st_t0 = __builtin_amdgcn_s_memtime();
 #define GST_STAMP(i)                                              \
   {                                                               \
@@ -96,8 +114,10 @@ __host__ __device__ constexpr int SL(int r, int s) { return r * (r + 1) / 2 + s;
   }
 #define GST_STAMP_FLUSH                                             \
   if (md.stamps && lane == 0)                                       \
-    for (int i_ = 0; i_ < 8; ++i_) md.stamps[(size_t)c * 8 + i_] += st_acc[i_];
+    for (int i_ = 0; i_ < 12; ++i_) md.stamps[(size_t)c * 12 + i_] += st_acc[i_];
 #else
+#define GST_SUB_BEGIN
+#define GST_SUB_END(i)
 #define GST_STAMP_DECL
 #define GST_STAMP_START
 #define GST_STAMP(i)
@@ -233,27 +253,27 @@ __device__ double gamma_mt(double a, const Rng& rng, uint32_t index, uint32_t ta
 // sum zraw^2 / a_kk (= the d^T Sigma^-1 d contribution).
 struct CholCtx {
   double* colq;   // [8][MP]
-  double* zraw;   // [MP]
-  double* apiv;   // [MP]
   int lane, p, q, raug;
   double mant, quad;
   int expo, fail;
+  // pivots a_kk and augmented-row entries a_{raug,k}, column k kept by lane k % 64 in
+  // slot k / 64 (registers: no LDS store on the step-to-step critical path)
+  double apr[2], zr[2];
 };
 
 template <int MT>
 __device__ __forceinline__ void chol_publish(const double (&L)[SL(MT, 0)], CholCtx& cc, int s) {
-  double* dst = cc.colq + 8 * MT * cc.q + cc.p;
+  double* dst = cc.colq + CQ(MT) * cc.q + cc.p;
 #pragma unroll
   for (int r = 0; r < MT; ++r)
     if (r >= s) dst[8 * r] = L[SL(r, s)];
 }
 
-// 1/a: hardware estimate + two Newton steps.
-__device__ __forceinline__ double rcp_nr(double a) {
-  double y = __builtin_amdgcn_rcp(a);
-  y = fma(y, fma(-a, y, 1.0), y);
-  y = fma(y, fma(-a, y, 1.0), y);
-  return y;
+// 1/a: hardware estimate (~2^-24) + one Newton step (~2e-15 relative, measured on
+// MI355X by tools/ubench/rcp_acc.hip); on every column step's critical path.
+__device__ __forceinline__ double rcp_nr1(double a) {
+  const double y = __builtin_amdgcn_rcp(a);
+  return fma(y, fma(-a, y, 1.0), y);
 }
 
 // Raw column k as seen by this lane: rows 8r+p (lr), rows 8r+q (lc), the augmented row
@@ -266,7 +286,7 @@ struct ColView {
 
 template <int MT, int K, int KK>
 __device__ __forceinline__ void chol_load(const CholCtx& cc, ColView<MT>& c) {
-  const double* col = cc.colq + 8 * MT * KK;
+  const double* col = cc.colq + CQ(MT) * KK;
   const double* cr = col + cc.p;
   const double* cq = col + cc.q;
 #pragma unroll
@@ -289,29 +309,35 @@ __device__ __forceinline__ void chol_step(double (&L)[SL(MT, 0)], CholCtx& cc,
   constexpr bool NEXT = k + 1 < KEND;
   cur.lr[K] = (8 * K + cc.p > k) ? cur.lr[K] : 0.0;
   cur.lc[K] = (8 * K + cc.q > k) ? cur.lc[K] : 0.0;
+  ColView<MT> nxt;
+  if constexpr (K1 < MT) {
+    // critical path: slot column K1 (holds column k+1).  The products lr*lc need only the
+    // LDS data, the FMA with 1/a_kk only the reciprocal: the two latencies overlap.
+    double t[MT];
+#pragma unroll
+    for (int r = K1; r < MT; ++r) t[r] = cur.lr[r] * cur.lc[K1];
+#pragma unroll
+    for (int r = K1; r < MT; ++r) L[SL(r, K1)] = fma(-t[r], cur.sk, L[SL(r, K1)]);
+    if constexpr (NEXT) {
+      chol_publish<MT>(L, cc, K1);
+      nxt.akk = rdlane(L[SL(K1, K1)], 9 * KK1);
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      chol_load<MT, K1, KK1>(cc, nxt);
+      nxt.sk = rcp_nr1(nxt.akk);
+    }
+  }
+  // off the critical path: bookkeeping and the rest of the trailing update
   cc.fail |= !(cur.akk > 0.0) ? 1 : 0;
   int e;
   const double mm = frexp(cur.akk, &e);
   cc.mant *= mm;
   cc.expo += e;
   cc.quad = fma(cur.zk * cur.zk, cur.sk, cc.quad);
-  cc.apiv[k] = cur.akk;
-  cc.zraw[k] = cur.zk;
+  cc.apr[k / 64] = (cc.lane == (k & 63)) ? cur.akk : cc.apr[k / 64];
+  cc.zr[k / 64] = (cc.lane == (k & 63)) ? cur.zk : cc.zr[k / 64];
   double lrs[MT];
 #pragma unroll
   for (int r = K; r < MT; ++r) lrs[r] = cur.lr[r] * cur.sk;
-  ColView<MT> nxt;
-  if constexpr (K1 < MT) {
-#pragma unroll
-    for (int r = K1; r < MT; ++r) L[SL(r, K1)] = fma(-lrs[r], cur.lc[K1], L[SL(r, K1)]);
-    if constexpr (NEXT) {
-      chol_publish<MT>(L, cc, K1);
-      nxt.akk = rdlane(L[SL(K1, K1)], 9 * KK1);
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      chol_load<MT, K1, KK1>(cc, nxt);
-      nxt.sk = rcp_nr(nxt.akk);
-    }
-  }
 #pragma unroll
   for (int s = K; s < MT; ++s) {
     if (s == K1 || (KK == 7 && s == K)) continue;  // slot column K is done when KK == 7
@@ -331,7 +357,7 @@ __device__ __forceinline__ void chol_range(double (&L)[SL(MT, 0)], CholCtx& cc) 
   c.akk = rdlane(L[SL(KLO, KLO)], 0);
   lds_order();
   chol_load<MT, KLO, 0>(cc, c);
-  c.sk = rcp_nr(c.akk);
+  c.sk = rcp_nr1(c.akk);
   chol_step<MT, KLO, 0, KEND>(L, cc, c);
   lds_order();
 }
@@ -349,7 +375,7 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
   constexpr int NS0 = SL(MT - K0, 0);  // S0 slots (r >= s >= K0)
   constexpr int TB_LD = 17;
   constexpr int WPB = wpb_for(MT, NS);
-  constexpr int LDSW = 8 * MP + 16 * TB_LD + 64 * NS + 7 * MP + 32 + 4 * 32;
+  constexpr int LDSW = 8 * CQ(MT) + 16 * TB_LD + 64 * NS + 7 * MP + 32 + 4 * 32;
   __shared__ double smem[WPB][LDSW];
   __shared__ double s0mem[WPB][NS0 * 64];   // Schur complement S0, [slot][lane]
 
@@ -358,9 +384,10 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
   const int c = blockIdx.x * WPB + wv;
   if (c >= C) return;
   const int p = lane >> 3, q = lane & 7;
+  GST_STAMP_DECL
 
   double* colq = smem[wv];            // [8][MP] published columns
-  double* tbuf = colq + 8 * MP;       // 16 x TB_LD Gram tile transpose
+  double* tbuf = colq + 8 * CQ(MT);   // 16 x TB_LD Gram tile transpose
   double* vbuf = tbuf + 16 * TB_LD;   // per-TOA scratch (weights), 64*NS
   double* bbuf = vbuf + 64 * NS;      // b, reference order
   double* phbuf = bbuf + MP;          // phi^-1 by internal index
@@ -396,6 +423,8 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
   for (int j = lane; j < MP; j += 64) phbuf[j] = 0.0;
 
   double rr[NS], s2[NS], al[NS], po[NS], yv[NS];
+  int cls[NS];
+  double wcls = 0.0;  // lane u < ncls: W_u of the current white block
   unsigned zb = 0u, vmask = 0u;
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
@@ -404,6 +433,7 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
     vmask |= ok ? (1u << s) : 0u;
     rr[s] = ok ? md.resid[t] : 0.0;
     s2[s] = ok ? md.sig2[t] : 1.0;
+    cls[s] = (ok && md.cidx) ? md.cidx[t] : -1;
     al[s] = ok ? st.alpha[(size_t)c * n + t] : 1.0;
     po[s] = ok ? st.pout[(size_t)c * n + t] : 0.0;
     const double zz = ok ? st.z[(size_t)c * n + t] : 0.0;
@@ -441,11 +471,47 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
     return ef * ef;
   };
 
-  // white-noise conditional likelihood (gibbs.py:262-284)
+  // white-noise conditional likelihood (gibbs.py:262-284).  Class path: TOAs with equal
+  // sigma share N0 = efac^2 sigma^2 + Q, so with a_t = alpha_t^z_t
+  //   sum_t log N_t = sum_t log a_t + sum_u c_u log N0_u,
+  //   sum_t y_t^2 / N_t = sum_u W_u / N0_u,   W_u = sum_{t in u} y_t^2 / a_t,
+  // where sum log a_t and W_u are fixed for the whole white block (b, alpha, z fixed).
+  double wcls_la = 0.0;   // sum_t log a_t
+  auto white_prep = [&]() __attribute__((always_inline)) {
+    if (md.ncls == 0) return;
+    double la = 0.0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      if ((vmask >> s) & 1u) la += ((zb >> s) & 1u) ? log(al[s]) : 0.0;
+    wcls_la = wave_sum(la);
+    for (int u = 0; u < md.ncls; ++u) {
+      double w = 0.0;
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+        if (((vmask >> s) & 1u) && cls[s] == u)
+          w += yv[s] * yv[s] / (((zb >> s) & 1u) ? al[s] : 1.0);
+      w = wave_sum(w);
+      if (lane == u) wcls = w;
+    }
+  };
   auto lnl_white = [&](const double (&xq)[4]) __attribute__((always_inline)) -> double {
     const double ef2 = efac2_of(xq);
     const double Q = exp(2.0 * pget(xq, md.idx_equad) * 2.302585092994045684);
+    if (md.ncls == 1) {  // uniform: no reduction
+      const double N0 = ef2 * md.csig2[0] + Q;
+      return -0.5 * ((wcls_la + md.ccount[0] * log(N0)) + rdlane(wcls, 0) / N0);
+    }
     double sl = 0.0, sq = 0.0;
+    if (md.ncls > 1) {
+      if (lane < md.ncls) {
+        const double N0 = ef2 * md.csig2[lane] + Q;
+        sl = md.ccount[lane] * log(N0);
+        sq = wcls / N0;
+      }
+      sl = wave_sum(sl) + wcls_la;
+      sq = wave_sum(sq);
+      return -0.5 * (sl + sq);
+    }
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       if (vmask & (1u << s)) {
@@ -516,6 +582,8 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
   // ---------------- matrix state ----------------
   double L[NSL];
   double ld_tm_m = 1.0, quad_tm = 0.0, logdetN = 0.0, rNr = 0.0;
+  double tm_apr = 1.0, tm_zr = 0.0;       // timing-model columns' pivots / aug entries
+  double f_apr[2] = {1.0, 1.0}, f_zr[2] = {0.0, 0.0};  // last factorisation's
   int ld_tm_e = 0, fail_tm = 0;
 
   // Gram: G = T_aug^T diag(1/N) T_aug on fp64 MFMA, then TM elimination -> S0.
@@ -538,6 +606,7 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
     logdetN = wave_sum(sl);
     rNr = wave_sum(sr);
     lds_order();
+    GST_SUB_BEGIN
     v4d acc[NTT];
 #pragma unroll
     for (int i = 0; i < NTT; ++i) acc[i] = (v4d){0.0, 0.0, 0.0, 0.0};
@@ -565,6 +634,7 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
 #pragma unroll
       for (int X = 0; X < NT; ++X) tv[X] = tn[X];
     }
+    GST_SUB_END(9)
     // MFMA C layout (col = lane&15, row = lane>>4 + 4 reg) -> cyclic register layout
 #pragma unroll
     for (int I = 0; I < NT; ++I) {
@@ -590,8 +660,12 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
       const int j = 8 * s + q;
       if (p == q) L[SL(s, s)] = (j < md.ntm) ? L[SL(s, s)] + md.tm_phiinv : 1.0;
     }
-    CholCtx cc{colq, zraw, apiv, lane, p, q, raug, 1.0, 0.0, 0, 0};
+    CholCtx cc{colq, lane, p, q, raug, 1.0, 0.0, 0, 0, {1.0, 1.0}, {0.0, 0.0}};
+    GST_SUB_END(10)
     chol_range<MT, 0, 8 * K0>(L, cc);
+    GST_SUB_END(11)
+    tm_apr = cc.apr[0];
+    tm_zr = cc.zr[0];
     ld_tm_m = cc.mant;
     ld_tm_e = cc.expo;
     quad_tm = cc.quad;
@@ -604,17 +678,16 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
 
   // b-marginalised likelihood at xq (gibbs.py:288-329); factor left in L.
   auto lnl_hyper = [&](const double (&xq)[4], int& failed) __attribute__((always_inline)) -> double {
+    GST_SUB_BEGIN
     const double lA = pget(xq, md.idx_logA);
     const double g = pget(xq, md.idx_gamma);
     // log phi_k = 2 lA ln10 - log(12 pi^2) + (g-3) log fyr - g log f_k + log df_k
     const double lc = 2.0 * lA * 2.302585092994045684 - md.log_12pi2 + (g - 3.0) * md.log_fyr;
-    double lsum = 0.0;
-    for (int f = lane; f < md.nf; f += 64) {
-      const double lphi = lc - g * md.lfreq[f] + md.ldf[f];
-      lsum += lphi;
-      phbuf[md.ntm_pad + f] = exp(-lphi);
-    }
-    const double logdet_phi = wave_sum(lsum) + md.logdet_phi_tm;
+    for (int f = lane; f < md.nf; f += 64)
+      phbuf[md.ntm_pad + f] = exp(-(lc - g * md.lfreq[f] + md.ldf[f]));
+    // sum_k log phi_k in closed form (no reduction on the critical path)
+    const double logdet_phi =
+        ((double)md.nf * lc - g * md.sum_lfreq + md.sum_ldf) + md.logdet_phi_tm;
     lds_order();
 #pragma unroll
     for (int r = K0; r < MT; ++r)
@@ -624,8 +697,14 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
         if (r == s && p == q) v += phbuf[8 * r + p];
         L[SL(r, s)] = v;
       }
-    CholCtx cc{colq, zraw, apiv, lane, p, q, raug, 1.0, 0.0, 0, 0};
+    CholCtx cc{colq, lane, p, q, raug, 1.0, 0.0, 0, 0, {tm_apr, 1.0}, {tm_zr, 0.0}};
+    GST_SUB_END(7)
     chol_range<MT, K0, RA>(L, cc);
+    GST_SUB_END(8)
+    f_apr[0] = cc.apr[0];
+    f_apr[1] = cc.apr[1];
+    f_zr[0] = cc.zr[0];
+    f_zr[1] = cc.zr[1];
     const double mant = cc.mant, quad = cc.quad;
     const int expo = cc.expo;
     failed = cc.fail | fail_tm;
@@ -638,7 +717,6 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
   };
 
   const bool rec_on = record_every > 0 && !eval_only;
-  GST_STAMP_DECL
   GST_STAMP_START
   compute_Tb();
   if (eval_only) nsweeps = 1;
@@ -678,6 +756,7 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
 
     // ---- white-noise MH block (gibbs.py:114-143); step -1 = the initial lnlike0
     if ((mask & 1u) || eval_only) {
+      white_prep();
       double l0 = 0.0, p0 = 0.0;
 #pragma unroll 1
       for (int step = -1; step < NWHITE; ++step) {
@@ -779,6 +858,15 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
         status |= 2;
       } else {
         // y_k = 1/sqrt(a_kk); z = L^-1 d has z_k = zraw_k * y_k; L_ik = a_ik * y_k
+#pragma unroll
+        for (int sl = 0; sl < 2; ++sl) {
+          const int j = 64 * sl + lane;
+          if (j < MP) {
+            apiv[j] = f_apr[sl];
+            zraw[j] = f_zr[sl];
+          }
+        }
+        lds_order();
         for (int j = lane; j < raug; j += 64) yinv[j] = rsqrt_nr(apiv[j]);
         lds_order();
         // rhs w = z + eta

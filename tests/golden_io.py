@@ -18,8 +18,8 @@ def fixture_names():
     return sorted(os.path.basename(p)[4:-4] for p in glob.glob(os.path.join(GOLDEN, "ref_*.npz")))
 
 
-def load_dataset(efac=False):
-    fn = "j1713_dataset_efac.npz" if efac else "j1713_dataset.npz"
+def load_dataset(efac=False, dataset="j1713"):
+    fn = "j1713_dataset_efac.npz" if efac else f"{dataset}_dataset.npz"
     d = np.load(os.path.join(GOLDEN, fn), allow_pickle=False)
     return PTA.from_arrays("J1713+0747", d["residuals"], d["toaerrs"], d["T"], d["Ffreqs"],
                            int(d["components"]), float(d["tm_weight"]),
@@ -30,7 +30,8 @@ def load_ref(name):
     d = dict(np.load(os.path.join(GOLDEN, f"ref_{name}.npz"), allow_pickle=False))
     d["kw"] = ast.literal_eval(str(d.pop("model_kw")))
     d["tape"] = {k[5:]: v for k, v in d.items() if k.startswith("tape_")}
-    d["pta"] = load_dataset(efac="efac" in name)
+    ds = name.split("_")[0] if name.split("_")[0] in ("sim", "twob") else "j1713"
+    d["pta"] = load_dataset(efac="efac" in name, dataset=ds)
     return d
 
 

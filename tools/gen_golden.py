@@ -310,6 +310,24 @@ def main():
     out["model_kw"] = np.array(repr(MODELS["beta"]))
     np.savez_compressed(os.path.join(OUTDIR, "ref_beta_efac_fixed.npz"), **out)
     print("efac fixed cond:", np.nanmax(out["tape_b_cond"]), file=sys.stderr)
+    # simulate_data.py-style pulsar: log-normal error bars (every TOA its own sigma)
+    sim, _ = gdata.simulate_data(seed=7, theta=0.1)
+    pta3 = PTA(sim)
+    np.savez_compressed(os.path.join(OUTDIR, "sim_dataset.npz"), **dataset_arrays(pta3, sim))
+    for name in ("beta", "t"):
+        out = run_one(pta3, name, MODELS[name], seed=777, niter=niter, x0=[4.33, -14.0, -7.6])
+        out["model_kw"] = np.array(repr(MODELS[name]))
+        np.savez_compressed(os.path.join(OUTDIR, f"ref_sim_{name}_fixed.npz"), **out)
+        print("sim", name, "cond:", np.nanmax(out["tape_b_cond"]), file=sys.stderr)
+    # two backends: J1713 epochs with alternating 40 ns / 100 ns error bars (2 noise classes)
+    tb = gdata.j1713(seed=1713, theta=0.05)
+    tb.toaerrs = np.where(np.arange(tb.n) % 2 == 0, 4e-8, 1e-7)
+    pta4 = PTA(tb)
+    np.savez_compressed(os.path.join(OUTDIR, "twob_dataset.npz"), **dataset_arrays(pta4, tb))
+    out = run_one(pta4, "uniform", MODELS["uniform"], seed=31, niter=niter,
+                  x0=[4.33, -14.0, -7.6])
+    out["model_kw"] = np.array(repr(MODELS["uniform"]))
+    np.savez_compressed(os.path.join(OUTDIR, "ref_twob_uniform_fixed.npz"), **out)
 
 
 if __name__ == "__main__":

@@ -16,7 +16,8 @@ from gibbs_student_t_amd.model import PTA  # noqa: E402
 from gibbs_student_t_amd.native import NativeSampler  # noqa: E402
 
 STAGES = ["record", "white MH", "Gram+TM elim", "hyper MH (11 chol)", "b draw",
-          "theta+z+alpha", "nu"]
+          "theta+z+alpha", "nu", "(hyper: phi + S0 load)", "(hyper: F chol)",
+          "(gram: MFMA loop)", "(gram: transpose+prior)", "(gram: TM chol)"]
 
 
 def main():
@@ -31,14 +32,14 @@ def main():
     ns.set_state(x=x0, z=np.ones((C, ns.n)), alpha=np.ones((C, ns.n)),
                  theta=np.full(C, 0.01), nu=np.full(C, 4.0))
     ns.sweep(20, seed=1)
-    buf = torch.zeros((C, 8), dtype=torch.int64, device=ns.tdev)
+    buf = torch.zeros((C, 12), dtype=torch.int64, device=ns.tdev)
     _abi.check(ns.lib, ns.lib.gst_debug_stamps(ns.ctx, ct.c_void_p(buf.data_ptr())),
                "gst_debug_stamps")
     ns.sweep(S, seed=1, sweep0=20)
     ns.synchronize()
     ms = ns.last_kernel_ms()
-    cyc = buf.cpu().numpy().astype(np.float64)[:, :7] / S
-    tot = cyc.sum(axis=1)
+    cyc = buf.cpu().numpy().astype(np.float64) / S
+    tot = cyc[:, :7].sum(axis=1)
     print(f"C={C} S={S} kernel {ms:.2f} ms = {ms / S * 1e3:.1f} us/sweep; "
           f"stamped cycles/sweep/chain median {np.median(tot):.0f}")
     for i, nm in enumerate(STAGES):
