@@ -266,6 +266,8 @@ int gst_model_set(void* ctx, const gst_model_desc* d) {
     md.hind[j] = j < d->n_hyper ? d->hyper_idx[j] : d->hyper_idx[0];
     md.wind[j] = j < d->n_white ? d->white_idx[j] : d->white_idx[0];
   }
+  md.lp_sum = 0.0;  // Python sum() order (gibbs.py:339)
+  for (int j = 0; j < P; ++j) md.lp_sum += md.lp_in[j];
   md.nh = d->n_hyper;
   md.nw = d->n_white;
   md.sig_h = 0.05 * d->n_hyper;

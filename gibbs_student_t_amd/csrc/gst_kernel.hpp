@@ -60,7 +60,7 @@ struct DevModel {
   int P;
   int idx_efac, idx_equad, idx_logA, idx_gamma;
   double efac_const;
-  double pmin[4], pmax[4], lp_in[4];
+  double pmin[4], pmax[4], lp_in[4], lp_sum;
   int hind[4], nh, wind[4], nw;
   double sig_h, sig_w;
   double mh_cdf[5], mh_size[5];
@@ -97,7 +97,7 @@ __host__ __device__ constexpr int CQ(int MT) { return 8 * MT + 2; }
 
 #ifdef GST_STAMPS
 #define GST_STAMP_DECL \
-  unsigned long long st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_t0 = 0, st_s0 = 0;
+  unsigned long long st_acc[16] = {0}, st_t0 = 0, st_s0 = 0;
 #define GST_SUB_BEGIN st_s0 = __builtin_amdgcn_s_memtime();
 #define GST_SUB_END(i)                                            \
   {                                                               \
@@ -114,7 +114,7 @@ __host__ __device__ constexpr int CQ(int MT) { return 8 * MT + 2; }
   }
 #define GST_STAMP_FLUSH                                             \
   if (md.stamps && lane == 0)                                       \
-    for (int i_ = 0; i_ < 12; ++i_) md.stamps[(size_t)c * 12 + i_] += st_acc[i_];
+    for (int i_ = 0; i_ < 16; ++i_) md.stamps[(size_t)c * 16 + i_] += st_acc[i_];
 #else
 #define GST_SUB_BEGIN
 #define GST_SUB_END(i)
@@ -188,12 +188,11 @@ __device__ __forceinline__ int iget4(const int (&a)[4], int i) {
   return i == 0 ? a[0] : (i == 1 ? a[1] : (i == 2 ? a[2] : a[3]));
 }
 
-// x + (xi * sigma) * scale exactly as numpy evaluates it (gibbs.py:97,130): no FMA, so the
-// chain positions match the reference bit for bit.
-__device__ __forceinline__ double mh_jump(double x, double xi, double sig, double scale) {
+// The jump (xi * sigma) * scale exactly as numpy evaluates it (gibbs.py:97,130): no FMA
+// contraction, so x + jump matches the reference bit for bit.
+__device__ __forceinline__ double mh_step(double xi, double sig, double scale) {
 #pragma clang fp contract(off)
-  const double step = (xi * sig) * scale;
-  return x + step;
+  return (xi * sig) * scale;
 }
 
 // numpy legacy binomial(1, p) given its uniform (inversion branch, random_binomial).
@@ -443,27 +442,48 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
   int status = 0;
   lds_order();
 
+  // y = r - T b (gibbs.py:213,237,272): 8 columns x NS TOA slots of loads in flight
   auto compute_Tb = [&]() __attribute__((always_inline)) {
+    double tb[NS];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      if (s < md.nslot_toa) {
-        double tb = 0.0;
-        const double* tc = md.Tcol + 64 * s + lane;
-#pragma unroll 4
-        for (int j = 0; j < m; ++j) tb = fma(tc[(size_t)j * npad], bbuf[j], tb);
-        yv[s] = rr[s] - tb;
-      } else {
-        yv[s] = 0.0;
+    for (int s = 0; s < NS; ++s) tb[s] = 0.0;
+    const int nsl = md.nslot_toa;
+    const double* tc = md.Tcol + lane;
+    int j = 0;
+#pragma unroll 1
+    for (; j + 8 <= m; j += 8) {
+      double tv[8][NS], bj[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+          tv[u][s] = tc[(size_t)(j + u) * npad + 64 * (s < nsl ? s : nsl - 1)];
+        bj[u] = bbuf[j + u];
       }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int s = 0; s < NS; ++s) tb[s] = fma(tv[u][s], bj[u], tb[s]);
     }
+#pragma unroll 1
+    for (; j < m; ++j) {
+      const double bjj = bbuf[j];
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+        tb[s] = fma(tc[(size_t)j * npad + 64 * (s < nsl ? s : nsl - 1)], bjj, tb[s]);
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) yv[s] = (s < nsl) ? rr[s] - tb[s] : 0.0;
   };
 
+  // sum of log-priors (gibbs.py:337-339): every prior is uniform, so the sum is the
+  // host-evaluated constant (Python sum order) when all parameters are in bounds, else -inf
   auto lnprior = [&](const double (&xq)[4]) __attribute__((always_inline)) -> double {
-    double s = 0.0;
+    bool in = true;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      if (j < P) s += (xq[j] >= md.pmin[j] && xq[j] <= md.pmax[j]) ? md.lp_in[j] : -INFINITY;
-    return s;
+      if (j < P) in = in && (xq[j] >= md.pmin[j]) && (xq[j] <= md.pmax[j]);
+    return in ? md.lp_sum : -INFINITY;
   };
 
   auto efac2_of = [&](const double (&xq)[4]) __attribute__((always_inline)) -> double {
@@ -494,9 +514,9 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
       if (lane == u) wcls = w;
     }
   };
-  auto lnl_white = [&](const double (&xq)[4]) __attribute__((always_inline)) -> double {
+  // Q = 10^(2 equad) is passed in: the MH steps carry it (Q_q = Q_x * 10^(2 delta)).
+  auto lnl_white = [&](const double (&xq)[4], double Q) __attribute__((always_inline)) -> double {
     const double ef2 = efac2_of(xq);
-    const double Q = exp(2.0 * pget(xq, md.idx_equad) * 2.302585092994045684);
     if (md.ncls == 1) {  // uniform: no reduction
       const double N0 = ef2 * md.csig2[0] + Q;
       return -0.5 * ((wcls_la + md.ccount[0] * log(N0)) + rdlane(wcls, 0) / N0);
@@ -553,30 +573,32 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
         k = k < nind - 1 ? k : nind - 1;
         par = (double)(white ? iget4(md.wind, k) : iget4(md.hind, k));
       }
-      mhv[4 * lane + 0] = us;
-      mhv[4 * lane + 1] = par;
-      mhv[4 * lane + 2] = xi;
-      mhv[4 * lane + 3] = la;
+      int cnt = 0;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) cnt += (md.mh_cdf[i] <= us) ? 1 : 0;
+      cnt = cnt < 4 ? cnt : 4;
+      const double scale = md.mh_size[0] * (cnt == 0) + md.mh_size[1] * (cnt == 1) +
+                           md.mh_size[2] * (cnt == 2) + md.mh_size[3] * (cnt == 3) +
+                           md.mh_size[4] * (cnt == 4);
+      const double delta = mh_step(xi, white ? md.sig_w : md.sig_h, scale);
+      mhv[4 * lane + 0] = par;
+      mhv[4 * lane + 1] = delta;
+      mhv[4 * lane + 2] = la;
+      mhv[4 * lane + 3] = exp(2.0 * delta * 2.302585092994045684);
     }
     lds_order();
   };
 
-  // MH proposal of global step gs (gibbs.py:90-97 / 123-130); returns log(u_accept)
-  auto propose = [&](const double (&xq)[4], double (&qv)[4], int gs, double sig)
+  // MH proposal of global step gs (gibbs.py:90-97 / 123-130): q = x with q[par] += delta;
+  // returns log(u_accept).  E receives 10^(2 delta) (equad moves rescale Q by it).
+  auto propose = [&](const double (&xq)[4], double (&qv)[4], int gs, double& E, int& par)
       __attribute__((always_inline)) -> double {
-    const double us = mhv[4 * gs + 0];
-    const int par = (int)mhv[4 * gs + 1];
-    const double xi = mhv[4 * gs + 2];
-    int cnt = 0;
+    par = (int)mhv[4 * gs + 0];
+    const double delta = mhv[4 * gs + 1];
+    E = mhv[4 * gs + 3];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) cnt += (md.mh_cdf[i] <= us) ? 1 : 0;
-    cnt = cnt < 4 ? cnt : 4;
-    const double scale = md.mh_size[0] * (cnt == 0) + md.mh_size[1] * (cnt == 1) +
-                         md.mh_size[2] * (cnt == 2) + md.mh_size[3] * (cnt == 3) +
-                         md.mh_size[4] * (cnt == 4);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) qv[j] = (j == par) ? mh_jump(xq[j], xi, sig, scale) : xq[j];
-    return mhv[4 * gs + 3];
+    for (int j = 0; j < 4; ++j) qv[j] = (j == par) ? xq[j] + delta : xq[j];
+    return mhv[4 * gs + 2];
   };
 
   // ---------------- matrix state ----------------
@@ -758,19 +780,25 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
     if ((mask & 1u) || eval_only) {
       white_prep();
       double l0 = 0.0, p0 = 0.0;
+      double Qx = exp(2.0 * pget(xv, md.idx_equad) * 2.302585092994045684);
 #pragma unroll 1
       for (int step = -1; step < NWHITE; ++step) {
-        double qv[4], luacc = 0.0;
+        double qv[4], luacc = 0.0, Qq = Qx;
         if (step < 0) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) qv[j] = xv[j];
         } else {
-          luacc = propose(xv, qv, step, md.sig_w);
+          double E;
+          int par;
+          luacc = propose(xv, qv, step, E, par);
+          if (par == md.idx_equad) Qq = Qx * E;
         }
         const double p1 = lnprior(qv);
         // out-of-prior: (l1 + -inf) - (l0 + p0) is -inf or NaN, never > log(u): skip lnL
         if (step >= 0 && p1 == -INFINITY) continue;
-        const double l1 = lnl_white(qv);
+        GST_SUB_BEGIN
+        const double l1 = lnl_white(qv, Qq);
+        GST_SUB_END(15)
         if (step < 0) {
           l0 = l1;
           p0 = p1;
@@ -785,6 +813,7 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
           for (int j = 0; j < 4; ++j) xv[j] = qv[j];
           l0 = l1;
           p0 = p1;
+          Qx = Qq;
         }
       }
     }
@@ -818,7 +847,9 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
 #pragma unroll
           for (int j = 0; j < 4; ++j) qv[j] = xv[j];
         } else {
-          luacc = propose(xv, qv, NWHITE + step, md.sig_h);
+          double E;
+          int par;
+          luacc = propose(xv, qv, NWHITE + step, E, par);
         }
         const double p1 = lnprior(qv);
         if (step >= 0 && step < NHYPER && p1 == -INFINITY) continue;
@@ -857,6 +888,7 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
       if (fb) {
         status |= 2;
       } else {
+        GST_SUB_BEGIN
         // y_k = 1/sqrt(a_kk); z = L^-1 d has z_k = zraw_k * y_k; L_ik = a_ik * y_k
 #pragma unroll
         for (int sl = 0; sl < 2; ++sl) {
@@ -895,6 +927,7 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
             wvec[j] = zraw[j] * yinv[j] + normal_from(rng, (uint32_t)j, TAG_BDRAW);
         }
         lds_order();
+        GST_SUB_END(12)
         // back substitution L^T v = w, descending columns:
         // v_k = (w_k - y_k * sum_{i>k} a_ik v_i) * y_k
         double vr[MT];
@@ -906,10 +939,13 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
           for (int kk = 7; kk >= 0; --kk) {
             const int k = 8 * K + kk;
             if (k >= raug) continue;
-            double part = 0.0;
+            double pe = 0.0, po2 = 0.0;
 #pragma unroll
-            for (int r = K; r < MT; ++r) part = fma(L[SL(r, K)], vr[r], part);
-            const double sk = col_sum(part, kk);
+            for (int r = K; r < MT; r += 2) {
+              pe = fma(L[SL(r, K)], vr[r], pe);
+              if (r + 1 < MT) po2 = fma(L[SL(r + 1, K)], vr[r + 1], po2);
+            }
+            const double sk = col_sum(pe + po2, kk);
             const double yk = yinv[k];
             const double vk = (wvec[k] - yk * sk) * yk;
             vr[K] = (p == kk) ? vk : vr[K];
@@ -917,9 +953,11 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
           }
         }
         lds_order();
+        GST_SUB_END(13)
         for (int j = lane; j < m; j += 64) bbuf[j] = xbuf[md.ref2int[j]];
         lds_order();
         compute_Tb();
+        GST_SUB_END(14)
       }
     }
 

@@ -17,7 +17,8 @@ from gibbs_student_t_amd.native import NativeSampler  # noqa: E402
 
 STAGES = ["record", "white MH", "Gram+TM elim", "hyper MH (11 chol)", "b draw",
           "theta+z+alpha", "nu", "(hyper: phi + S0 load)", "(hyper: F chol)",
-          "(gram: MFMA loop)", "(gram: transpose+prior)", "(gram: TM chol)"]
+          "(gram: MFMA loop)", "(gram: transpose+prior)", "(gram: TM chol)",
+          "(b: yinv + rhs)", "(b: back-subst)", "(b: T b)", "(white: lnL evals)"]
 
 
 def main():
@@ -32,7 +33,7 @@ def main():
     ns.set_state(x=x0, z=np.ones((C, ns.n)), alpha=np.ones((C, ns.n)),
                  theta=np.full(C, 0.01), nu=np.full(C, 4.0))
     ns.sweep(20, seed=1)
-    buf = torch.zeros((C, 12), dtype=torch.int64, device=ns.tdev)
+    buf = torch.zeros((C, 16), dtype=torch.int64, device=ns.tdev)
     _abi.check(ns.lib, ns.lib.gst_debug_stamps(ns.ctx, ct.c_void_p(buf.data_ptr())),
                "gst_debug_stamps")
     ns.sweep(S, seed=1, sweep0=20)
