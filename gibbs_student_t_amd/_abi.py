@@ -18,8 +18,10 @@ STAGE_ALL = 0x7F
 STAGE_B_FORCE = 0x80
 TAPE_WHITE, TAPE_HYPER, TAPE_DELTA = 0, 80, 120
 
+ABI_VERSION = 2
 EXPORTS = ("gst_version", "gst_tape_stride", "gst_last_error", "gst_ctx_create",
-           "gst_ctx_destroy", "gst_model_set", "gst_sweep", "gst_eval_lnlike", "gst_sync",
+           "gst_ctx_destroy", "gst_model_set", "gst_model_set_batch", "gst_model_info",
+           "gst_sweep", "gst_eval_lnlike", "gst_sync",
            "gst_last_sweep_ms", "gst_debug_stamps")
 
 _P = ct.POINTER
@@ -51,7 +53,7 @@ class ModelDesc(ct.Structure):
 class State(ct.Structure):
     _fields_ = [("x", ct.c_void_p), ("b", ct.c_void_p), ("z", ct.c_void_p),
                 ("alpha", ct.c_void_p), ("pout", ct.c_void_p), ("theta", ct.c_void_p),
-                ("nu", ct.c_void_p), ("status", ct.c_void_p)]
+                ("nu", ct.c_void_p), ("status", ct.c_void_p), ("dataset", ct.c_void_p)]
 
 
 class Records(ct.Structure):
@@ -96,6 +98,8 @@ def load(path: str | None = None):
     lib.gst_ctx_create.argtypes = [ct.c_int, _P(ct.c_void_p)]
     lib.gst_ctx_destroy.argtypes = [ct.c_void_p]
     lib.gst_model_set.argtypes = [ct.c_void_p, _P(ModelDesc)]
+    lib.gst_model_set_batch.argtypes = [ct.c_void_p, _P(ModelDesc), ct.c_int]
+    lib.gst_model_info.argtypes = [ct.c_void_p, _P(ct.c_int), _P(ct.c_int), _P(ct.c_int)]
     lib.gst_sweep.argtypes = [ct.c_void_p, _P(State), _P(Records), _P(Tape), ct.c_int,
                               ct.c_int, ct.c_longlong, ct.c_int, ct.c_uint, ct.c_ulonglong,
                               ct.c_longlong, ct.c_void_p]
@@ -107,6 +111,8 @@ def load(path: str | None = None):
     for name in EXPORTS:
         if name != "gst_version":
             getattr(lib, name).restype = ct.c_int
+    if lib.gst_version() != ABI_VERSION:
+        raise GstNativeError(f"{p}: ABI version {lib.gst_version()} != {ABI_VERSION}; rebuild")
     if path is None:
         _lib = lib
     return lib

@@ -7,6 +7,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -33,7 +34,9 @@ int fail(const std::string& msg) {
 struct Ctx {
   int device = 0;
   bool has_model = false;
-  gst::DevModel md{};
+  std::vector<gst::DevModel> hmd;  // host copies, one per dataset
+  gst::DevModel* dmd = nullptr;    // device array [nd] (in allocs)
+  int nd = 0, nmax = 0, m = 0, raug = 0;
   int MT = 0, NS = 0, K0 = 0, WPB = 4;
   std::vector<void*> allocs;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -52,10 +55,13 @@ int upload(Ctx* cx, const void* host, size_t bytes, void** dev) {
 void free_model(Ctx* cx) {
   for (void* p : cx->allocs) (void)hipFree(p);
   cx->allocs.clear();
+  cx->hmd.clear();
+  cx->dmd = nullptr;
+  cx->nd = 0;
   cx->has_model = false;
 }
 
-typedef void (*kfn_t)(const gst::DevModel, const gst::DevState, const gst::DevRec,
+typedef void (*kfn_t)(const gst::DevModel*, const gst::DevState, const gst::DevRec,
                       const gst::DevTape, int, int, long long, int, unsigned,
                       unsigned long long, long long, int, double*, double*);
 
@@ -118,33 +124,13 @@ int gst_ctx_destroy(void* ctx) {
   return 0;
 }
 
-int gst_model_set(void* ctx, const gst_model_desc* d) {
-  Ctx* cx = static_cast<Ctx*>(ctx);
-  if (!cx || !d) return fail("gst_model_set: null argument");
-  HIP_OK(hipSetDevice(cx->device));
+// Pack one dataset's constants (shapes already validated) into device buffers owned by cx.
+static int pack_dataset(Ctx* cx, const gst_model_desc* d, gst::DevModel& md) {
   const int n = d->n, m = d->m, nf = d->nfourier, ntm = d->ntm, P = d->nparams;
-  if (n <= 0 || m != nf + ntm || nf <= 0 || ntm < 0) return fail("gst_model_set: bad sizes");
-  if (P < 1 || P > 4) return fail("gst_model_set: nparams must be 1..4");
-  if (d->idx_equad < 0 || d->idx_log10_A < 0 || d->idx_gamma < 0)
-    return fail("gst_model_set: equad, log10_A and gamma parameters are required");
-  if (d->n_hyper < 1 || d->n_hyper > 4 || d->n_white < 1 || d->n_white > 4)
-    return fail("gst_model_set: bad hyper/white index sets");
   const int ntm_pad = round_up(ntm > 0 ? ntm : 1, 8);
   const int raug = ntm_pad + nf;
   const int mpad = round_up(raug + 1, 16);
-  const int MT = mpad / 8, K0 = ntm_pad / 8;
-  const int NS = (n + 63) / 64 <= 2 ? 2 : ((n + 63) / 64 <= 3 ? 3 : 4);
   const int npad = 64 * ((n + 63) / 64);
-  if (round_up(n, 4) > 64 * NS) return fail("gst_model_set: n too large for TOA slots");
-  if (!pick(MT, NS, K0, raug, false)) {
-    char b[200];
-    std::snprintf(b, sizeof b,
-                  "gst_model_set: no kernel instance for MT=%d NS=%d K0=%d RA=%d (n=%d m=%d "
-                  "nfourier=%d ntm=%d); add a GST_CASE in gst.hip",
-                  MT, NS, K0, raug, n, m, nf, ntm);
-    return fail(b);
-  }
-  free_model(cx);
 
   // internal column order: [TM | pad | Fourier | r | pad]
   std::vector<int> ref2int(m), int2ref(mpad, -1);
@@ -212,7 +198,7 @@ int gst_model_set(void* ctx, const gst_model_desc* d) {
     dfB[k] = d->df_B[k];
   }
 
-  gst::DevModel md{};
+  md = gst::DevModel{};
   void* ptr;
   if (upload(cx, Tmf.data(), Tmf.size() * 8, &ptr)) return -1;
   md.Tmf = (const double*)ptr;
@@ -298,12 +284,98 @@ int gst_model_set(void* ctx, const gst_model_desc* d) {
   md.logdet_phi_tm = ntm * std::log(d->tm_weight);
   md.log_fyr = std::log(1.0 / (365.25 * 86400.0));
   md.log_12pi2 = std::log(12.0) + 2.0 * std::log(M_PI);
-  cx->md = md;
+  return 0;
+}
+
+static int check_desc(const gst_model_desc* d) {
+  const int n = d->n, m = d->m, nf = d->nfourier, ntm = d->ntm, P = d->nparams;
+  if (n <= 0 || m != nf + ntm || nf <= 0 || ntm < 0) return fail("gst_model_set: bad sizes");
+  if (P < 1 || P > 4) return fail("gst_model_set: nparams must be 1..4");
+  if (d->idx_equad < 0 || d->idx_log10_A < 0 || d->idx_gamma < 0)
+    return fail("gst_model_set: equad, log10_A and gamma parameters are required");
+  if (d->n_hyper < 1 || d->n_hyper > 4 || d->n_white < 1 || d->n_white > 4)
+    return fail("gst_model_set: bad hyper/white index sets");
+  if (!d->T || !d->residuals || !d->toaerrs || !d->ffreqs || !d->pmin || !d->pmax ||
+      !d->hyper_idx || !d->white_idx || !d->df_A || !d->df_B)
+    return fail("gst_model_set: null array in model descriptor");
+  return 0;
+}
+
+// Datasets of one batch share the sampler structure: basis shape, parameter roles and the
+// MH index sets.  n (ragged run_sims datasets), the data and the outlier model may differ.
+static int same_structure(const gst_model_desc* a, const gst_model_desc* b) {
+  if (a->m != b->m || a->nfourier != b->nfourier || a->ntm != b->ntm ||
+      a->nparams != b->nparams || a->idx_efac != b->idx_efac || a->idx_equad != b->idx_equad ||
+      a->idx_log10_A != b->idx_log10_A || a->idx_gamma != b->idx_gamma ||
+      a->n_hyper != b->n_hyper || a->n_white != b->n_white)
+    return 0;
+  for (int j = 0; j < a->n_hyper; ++j)
+    if (a->hyper_idx[j] != b->hyper_idx[j]) return 0;
+  for (int j = 0; j < a->n_white; ++j)
+    if (a->white_idx[j] != b->white_idx[j]) return 0;
+  return 1;
+}
+
+int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
+  Ctx* cx = static_cast<Ctx*>(ctx);
+  if (!cx || !descs || nd <= 0) return fail("gst_model_set_batch: null argument");
+  HIP_OK(hipSetDevice(cx->device));
+  int nmax = 0;
+  for (int i = 0; i < nd; ++i) {
+    if (check_desc(&descs[i])) return -1;
+    if (!same_structure(&descs[0], &descs[i]))
+      return fail("gst_model_set_batch: datasets differ in basis shape, parameters or MH "
+                  "index sets (dataset " + std::to_string(i) + ")");
+    nmax = std::max(nmax, descs[i].n);
+  }
+  const gst_model_desc* d = &descs[0];
+  const int nf = d->nfourier, ntm = d->ntm, m = d->m;
+  const int ntm_pad = round_up(ntm > 0 ? ntm : 1, 8);
+  const int raug = ntm_pad + nf;
+  const int mpad = round_up(raug + 1, 16);
+  const int MT = mpad / 8, K0 = ntm_pad / 8;
+  const int nsl = (nmax + 63) / 64;
+  const int NS = nsl <= 2 ? 2 : (nsl <= 3 ? 3 : 4);
+  if (round_up(nmax, 4) > 64 * NS) return fail("gst_model_set: n too large for TOA slots");
+  if (!pick(MT, NS, K0, raug, false)) {
+    char b[200];
+    std::snprintf(b, sizeof b,
+                  "gst_model_set: no kernel instance for MT=%d NS=%d K0=%d RA=%d (n=%d m=%d "
+                  "nfourier=%d ntm=%d); add a GST_CASE in gst.hip",
+                  MT, NS, K0, raug, nmax, m, nf, ntm);
+    return fail(b);
+  }
+  free_model(cx);
+  std::vector<gst::DevModel> hmd(nd);
+  for (int i = 0; i < nd; ++i)
+    if (pack_dataset(cx, &descs[i], hmd[i])) {
+      free_model(cx);
+      return -1;
+    }
+  void* ptr;
+  if (upload(cx, hmd.data(), hmd.size() * sizeof(gst::DevModel), &ptr)) return -1;
+  cx->dmd = (gst::DevModel*)ptr;
+  cx->hmd = hmd;
+  cx->nd = nd;
+  cx->nmax = nmax;
   cx->MT = MT;
   cx->NS = NS;
   cx->K0 = K0;
+  cx->raug = raug;
+  cx->m = m;
   cx->WPB = gst::wpb_for(MT, NS);
   cx->has_model = true;
+  return 0;
+}
+
+int gst_model_set(void* ctx, const gst_model_desc* d) { return gst_model_set_batch(ctx, d, 1); }
+
+int gst_model_info(void* ctx, int* ndatasets, int* nmax, int* tape_stride) {
+  Ctx* cx = static_cast<Ctx*>(ctx);
+  if (!cx || !cx->has_model) return fail("gst_model_info: no model set");
+  if (ndatasets) *ndatasets = cx->nd;
+  if (nmax) *nmax = cx->nmax;
+  if (tape_stride) *tape_stride = gst_tape_stride(cx->nmax, cx->m);
   return 0;
 }
 
@@ -317,19 +389,22 @@ static int launch(Ctx* cx, const gst_state* s, const gst_records* r, const gst_t
   if (C <= 0) return 0;
   HIP_OK(hipSetDevice(cx->device));
   const bool tape = tp && tp->data;
-  kfn_t k = pick(cx->MT, cx->NS, cx->K0, cx->md.raug, tape);
+  kfn_t k = pick(cx->MT, cx->NS, cx->K0, cx->raug, tape);
   if (!k) return fail("gst: no kernel instance");
-  gst::DevState ds{s->x, s->b, s->z, s->alpha, s->pout, s->theta, s->nu, s->status};
+  if (!s->dataset && cx->nd > 1)
+    return fail("gst: the model has several datasets: state.dataset must be set");
+  gst::DevState ds{s->x,     s->b,  s->z,      s->alpha,  s->pout,
+                   s->theta, s->nu, s->status, s->dataset, cx->nmax, cx->nd};
   gst::DevRec dr{};
   if (r) dr = gst::DevRec{r->x, r->b, r->z, r->alpha, r->pout, r->theta, r->nu, r->nrec};
   else record_every = 0;
-  if (tape && tp->stride != gst_tape_stride(cx->md.n, cx->md.m))
+  if (tape && tp->stride != gst_tape_stride(cx->nmax, cx->m))
     return fail("gst: tape stride mismatch");
   gst::DevTape dt{tape ? tp->data : nullptr, tape ? tp->stride : 0};
   const dim3 grid((C + cx->WPB - 1) / cx->WPB), block(64 * cx->WPB);
   hipStream_t st = (hipStream_t)stream;
   HIP_OK(hipEventRecord(cx->ev0, st));
-  hipLaunchKernelGGL(k, grid, block, 0, st, cx->md, ds, dr, dt, C, nsweeps, sweep0,
+  hipLaunchKernelGGL(k, grid, block, 0, st, cx->dmd, ds, dr, dt, C, nsweeps, sweep0,
                      record_every, mask, seed, chain0, eval_only, ow, oh);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(cx->ev1, st));
@@ -358,7 +433,9 @@ int gst_debug_stamps(void* ctx, unsigned long long* dev_buf) {
   Ctx* cx = static_cast<Ctx*>(ctx);
   if (!cx || !cx->has_model) return fail("gst_debug_stamps: no model");
 #ifdef GST_STAMPS
-  cx->md.stamps = dev_buf;
+  for (auto& h : cx->hmd) h.stamps = dev_buf;
+  HIP_OK(hipMemcpy(cx->dmd, cx->hmd.data(), cx->hmd.size() * sizeof(gst::DevModel),
+                   hipMemcpyHostToDevice));
   return 0;
 #else
   (void)dev_buf;

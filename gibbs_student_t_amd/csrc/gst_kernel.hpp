@@ -75,6 +75,9 @@ struct DevModel {
 struct DevState {
   double *x, *b, *z, *alpha, *pout, *theta, *nu;
   int* status;
+  const int* dataset;  // [C] dataset of each chain (null: every chain uses dataset 0)
+  int nst;             // row stride of the per-TOA arrays (max n over the datasets)
+  int nd;              // number of datasets
 };
 struct DevRec {
   double *x, *b, *z, *alpha, *pout, *theta, *nu;
@@ -363,7 +366,7 @@ __device__ __forceinline__ void chol_range(double (&L)[SL(MT, 0)], CholCtx& cc) 
 
 template <int MT, int NS, int K0, int RA, bool TAPE>
 __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
-    gst_sweep_kernel(const DevModel md, const DevState st, const DevRec rec, const DevTape tape,
+    gst_sweep_kernel(const DevModel* __restrict__ mds, const DevState st, const DevRec rec, const DevTape tape,
                      int C, int nsweeps, long long sweep0, int record_every, unsigned mask,
                      unsigned long long seed, long long chain0, int eval_only, double* out_w,
                      double* out_h) {
@@ -379,9 +382,18 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
   __shared__ double s0mem[WPB][NS0 * 64];   // Schur complement S0, [slot][lane]
 
   const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = blockIdx.x * WPB + wv;
   if (c >= C) return;
+  // the chain's dataset (run_sims grids batch many datasets x models per launch): every
+  // field of md is wave-uniform, so it is read with scalar loads
+  const int ds = st.dataset ? __builtin_amdgcn_readfirstlane(st.dataset[c]) : 0;
+  if ((unsigned)ds >= (unsigned)st.nd) {  // bad index: flag the chain, touch nothing else
+    if (lane == 0 && st.status) st.status[c] |= 4;
+    return;
+  }
+  const DevModel& md = mds[ds];
+  const int nst = st.nst;
   const int p = lane >> 3, q = lane & 7;
   GST_STAMP_DECL
 
@@ -433,9 +445,9 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
     rr[s] = ok ? md.resid[t] : 0.0;
     s2[s] = ok ? md.sig2[t] : 1.0;
     cls[s] = (ok && md.cidx) ? md.cidx[t] : -1;
-    al[s] = ok ? st.alpha[(size_t)c * n + t] : 1.0;
-    po[s] = ok ? st.pout[(size_t)c * n + t] : 0.0;
-    const double zz = ok ? st.z[(size_t)c * n + t] : 0.0;
+    al[s] = ok ? st.alpha[(size_t)c * nst + t] : 1.0;
+    po[s] = ok ? st.pout[(size_t)c * nst + t] : 0.0;
+    const double zz = ok ? st.z[(size_t)c * nst + t] : 0.0;
     zb |= (zz != 0.0) ? (1u << s) : 0u;
     yv[s] = 0.0;
   }
@@ -760,9 +772,9 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
         for (int s = 0; s < NS; ++s) {
           const int t = 64 * s + lane;
           if (vmask & (1u << s)) {
-            if (rec.z) rec.z[base * n + t] = (double)((zb >> s) & 1u);
-            if (rec.alpha) rec.alpha[base * n + t] = al[s];
-            if (rec.pout) rec.pout[base * n + t] = po[s];
+            if (rec.z) rec.z[base * nst + t] = (double)((zb >> s) & 1u);
+            if (rec.alpha) rec.alpha[base * nst + t] = al[s];
+            if (rec.pout) rec.pout[base * nst + t] = po[s];
           }
         }
         if (lane == 0) {
@@ -1028,7 +1040,7 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
             const double top = ((yv[s] * yv[s]) * zf / N0 + nu) / 2.0;
             double G;
             if (TAPE) {
-              G = tp[TP_DELTA + m + 1 + n + t];
+              G = tp[TP_DELTA + m + 1 + nst + t];
             } else {
               G = gamma_mt((zf + nu) / 2.0, rng, (uint32_t)t, TAG_ALPHA);
             }
@@ -1055,7 +1067,7 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
       lds_order();
       double u;
       if (TAPE) {
-        u = tp[TP_DELTA + m + 1 + 2 * n];
+        u = tp[TP_DELTA + m + 1 + 2 * nst];
       } else {
         double unused;
         rng.uniform2(0u, TAG_DF, u, unused);
@@ -1097,9 +1109,9 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
   for (int s = 0; s < NS; ++s) {
     const int t = 64 * s + lane;
     if (vmask & (1u << s)) {
-      st.z[(size_t)c * n + t] = (double)((zb >> s) & 1u);
-      st.alpha[(size_t)c * n + t] = al[s];
-      st.pout[(size_t)c * n + t] = po[s];
+      st.z[(size_t)c * nst + t] = (double)((zb >> s) & 1u);
+      st.alpha[(size_t)c * nst + t] = al[s];
+      st.pout[(size_t)c * nst + t] = po[s];
     }
   }
   if (lane == 0) {

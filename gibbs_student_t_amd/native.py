@@ -81,7 +81,13 @@ def model_desc(pta, cfg: dict):
 
 
 class NativeSampler:
-    """One HIP context + model + a batch of C chains resident on one GPU."""
+    """One HIP context + model + a batch of C chains resident on one GPU.
+
+    ``pta``/``cfg`` may be lists: a batch of datasets (e.g. the run_sims.py grid of
+    simulated pulsars x outlier models) sharing the basis shape and parameter set; each
+    chain then names its dataset through ``alloc(C, dataset=...)``.  Per-TOA state and
+    record arrays are laid out with row stride ``self.n`` = the largest n of the batch.
+    """
 
     def __init__(self, pta, cfg: dict, device: int = 0):
         torch = _torch()
@@ -90,25 +96,50 @@ class NativeSampler:
             raise _abi.GstNativeError("no HIP device visible: the sampler runs only on GPU")
         self.device = int(device)
         self.tdev = torch.device("cuda", self.device)
+        ptas = list(pta) if isinstance(pta, (list, tuple)) else [pta]
+        cfgs = list(cfg) if isinstance(cfg, (list, tuple)) else [cfg] * len(ptas)
+        if len(cfgs) != len(ptas):
+            raise ValueError("one cfg per dataset (or a single shared cfg)")
         ctx = ct.c_void_p()
         _abi.check(self.lib, self.lib.gst_ctx_create(self.device, ct.byref(ctx)),
                    "gst_ctx_create")
         self.ctx = ctx
-        self.pta = pta
-        self.cfg = dict(cfg)
-        desc, keep = model_desc(pta, cfg)
-        _abi.check(self.lib, self.lib.gst_model_set(self.ctx, ct.byref(desc)), "gst_model_set")
-        self.n, self.m = pta.T.shape
-        self.P = len(pta.params)
-        self.stride = int(self.lib.gst_tape_stride(self.n, self.m))
+        self.ptas, self.cfgs = ptas, [dict(c) for c in cfgs]
+        self.pta, self.cfg = ptas[0], self.cfgs[0]
+        descs, self._keep = [], []
+        for p_, c_ in zip(ptas, cfgs):
+            d, k = model_desc(p_, c_)
+            descs.append(d)
+            self._keep.append(k)
+        arr = (_abi.ModelDesc * len(descs))(*descs)
+        _abi.check(self.lib, self.lib.gst_model_set_batch(self.ctx, arr, len(descs)),
+                   "gst_model_set_batch")
+        nd, nmax, stride = ct.c_int(), ct.c_int(), ct.c_int()
+        _abi.check(self.lib, self.lib.gst_model_info(self.ctx, ct.byref(nd), ct.byref(nmax),
+                                                     ct.byref(stride)), "gst_model_info")
+        self.ndatasets = nd.value
+        self.n_of = [int(p_.T.shape[0]) for p_ in ptas]
+        self.n, self.m = nmax.value, int(ptas[0].T.shape[1])
+        self.P = len(ptas[0].params)
+        self.stride = stride.value
         self.C = 0
         self.state = None
+        self.dataset = None
 
     # ---- state ---------------------------------------------------------------------
-    def alloc(self, C: int):
+    def alloc(self, C: int, dataset=None):
+        """Allocate C chains; ``dataset[c]`` is chain c's dataset index (default all 0)."""
         torch = _torch()
         f64 = dict(dtype=torch.float64, device=self.tdev)
         self.C = int(C)
+        ds = np.zeros(C, dtype=np.int32) if dataset is None else \
+            np.asarray(dataset, dtype=np.int32).reshape(C)
+        if ds.size and (ds.min() < 0 or ds.max() >= self.ndatasets):
+            raise ValueError(f"dataset indices must lie in [0, {self.ndatasets})")
+        if dataset is None and self.ndatasets > 1:
+            raise ValueError("several datasets: pass dataset= to alloc")
+        self.dataset_host = ds
+        self.dataset = torch.as_tensor(ds).to(self.tdev)
         self.state = {
             "x": torch.zeros((C, self.P), **f64), "b": torch.zeros((C, self.m), **f64),
             "z": torch.zeros((C, self.n), **f64), "alpha": torch.ones((C, self.n), **f64),
@@ -133,7 +164,8 @@ class NativeSampler:
     def _state_struct(self):
         s = self.state
         return _abi.State(*(ct.c_void_p(s[k].data_ptr()) for k in STATE_KEYS),
-                          ct.c_void_p(s["status"].data_ptr()))
+                          ct.c_void_p(s["status"].data_ptr()),
+                          ct.c_void_p(self.dataset.data_ptr()))
 
     def alloc_records(self, nrec: int, keys=STATE_KEYS):
         torch = _torch()
@@ -202,8 +234,11 @@ class NativeSampler:
             pass
 
 
-def pack_tape(ref_tape: dict, sweeps, n: int, m: int, stride: int):
-    """Golden-fixture tape (tools/gen_golden.py fields) -> [len(sweeps), stride] rows."""
+def pack_tape(ref_tape: dict, sweeps, n: int, m: int, stride: int, nst: int | None = None):
+    """Golden-fixture tape (tools/gen_golden.py fields) -> [len(sweeps), stride] rows.
+
+    ``nst`` is the per-TOA row stride of the launch (the batch's largest n; default n)."""
+    nst = n if nst is None else int(nst)
     rows = np.zeros((len(sweeps), stride))
     for k, i in enumerate(sweeps):
         row = rows[k]
@@ -215,6 +250,6 @@ def pack_tape(ref_tape: dict, sweeps, n: int, m: int, stride: int):
         row[o:o + m] = np.nan_to_num(ref_tape["b_delta"][i])
         row[o + m] = ref_tape["beta"][i]
         row[o + m + 1:o + m + 1 + n] = ref_tape["z_u"][i]
-        row[o + m + 1 + n:o + m + 1 + 2 * n] = ref_tape["gamma"][i]
-        row[o + m + 1 + 2 * n] = ref_tape["df_u"][i]
+        row[o + m + 1 + nst:o + m + 1 + nst + n] = ref_tape["gamma"][i]
+        row[o + m + 1 + 2 * nst] = ref_tape["df_u"][i]
     return rows

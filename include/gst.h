@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GST_ABI_VERSION 1
+#define GST_ABI_VERSION 2
 
 /* Outlier model kind: Gibbs(model=...) (gibbs.py:9,32,187-226). */
 enum gst_outlier_model {
@@ -83,9 +83,12 @@ typedef struct gst_model_desc {
   const double* df_B;      /* 30: n*gammaln(nu/2) */
 } gst_model_desc;
 
-/* Per-chain state, device pointers, chain-major.  x[C*P], b[C*m], z/alpha/pout[C*n],
- * theta/nu[C]; status[C] may be NULL (bit 0: Cholesky failure seen in the hyper block,
- * bit 1: b-draw factorisation failed and b was kept). */
+/* Per-chain state, device pointers, chain-major.  x[C*P], b[C*m], z/alpha/pout[C*nmax]
+ * (nmax = largest n of the model's datasets; TOAs t >= n of a chain's dataset are never
+ * touched), theta/nu[C]; status[C] may be NULL (bit 0: Cholesky failure seen in the hyper
+ * block, bit 1: b-draw factorisation failed and b was kept, bit 2: dataset index out of
+ * range -- the chain was not run).  dataset[C] gives each chain's dataset index into the
+ * batch passed to gst_model_set_batch; it may be NULL when there is one dataset. */
 typedef struct gst_state {
   double* x;
   double* b;
@@ -95,10 +98,12 @@ typedef struct gst_state {
   double* theta;
   double* nu;
   int* status;
+  const int* dataset;
 } gst_state;
 
 /* Chain records (Gibbs.sample's chain/bchain/zchain/... arrays, gibbs.py:344-361):
- * device pointers shaped [C][nrec][...]; any pointer may be NULL to skip that array.
+ * device pointers shaped [C][nrec][...] (per-TOA arrays [C][nrec][nmax]); any pointer may
+ * be NULL to skip that array.
  * Sweep i of a launch is stored at record (i / record_every) when i % record_every == 0,
  * holding the state at the START of the sweep, as the reference does (gibbs.py:355-361). */
 typedef struct gst_records {
@@ -113,7 +118,7 @@ typedef struct gst_records {
 } gst_records;
 
 /* Injected-variate tape (parity mode), device pointer [C][nsweeps][stride] fp64 with
- * stride = gst_tape_stride(n, m).  Per chain-sweep layout:
+ * stride = gst_tape_stride(nmax, m) (n = nmax below).  Per chain-sweep layout:
  *   [0,80)   white MH step s: u_scale, param index, jump normal, accept uniform
  *   [80,120) hyper MH step s: same
  *   [120,120+m)  b draw term Delta = U S^-1/2 xi in reference order
@@ -132,6 +137,17 @@ int gst_ctx_destroy(void* ctx);
 
 /* Upload model constants (replaces the pta object, gibbs.py:29-35). */
 int gst_model_set(void* ctx, const gst_model_desc* desc);
+
+/* Upload a batch of `ndatasets` models at once (one Gibbs object per dataset x outlier
+ * model in run_sims.py:80-113, e.g. the outlier / no_outlier pair of simulate_data.py at
+ * several thetas, each under the five outlier models).  The descriptors must agree in
+ * m, nfourier, ntm, nparams, parameter roles and hyper/white index sets; n, the data,
+ * priors and the outlier-model options may differ.  Chains pick their dataset through
+ * gst_state.dataset. */
+int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int ndatasets);
+
+/* Number of datasets, largest n (row stride of per-TOA state/records) and tape stride. */
+int gst_model_info(void* ctx, int* ndatasets, int* nmax, int* tape_stride);
 
 /* Run `nsweeps` Gibbs sweeps for chains [0, nchains) (Gibbs.sample's loop body,
  * gibbs.py:354-380).  `tape` NULL or tape->data NULL -> on-device Philox4x32-10 variates

@@ -1,0 +1,126 @@
+"""Dataset batches on the GPU: many (dataset, outlier model) pairs in one launch.
+
+run_sims.py:80-113 runs every simulated pulsar (outlier / no_outlier twin of
+simulate_data.py, whose n differ) under five outlier models.  The sampler batches such a
+grid into one launch: each chain names its dataset (gst_state.dataset), per-TOA arrays use
+the batch's largest n as row stride.  Parity: every chain of a batch must reproduce its own
+reference fixture (same tolerances as test_gpu_parity.py) and, in Philox mode, be bitwise
+identical to a launch of its dataset alone.
+"""
+import numpy as np
+import pytest
+
+from golden_io import fixture_names, load_ref, sweep_state
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a HIP device", allow_module_level=True)
+
+from gibbs_student_t_amd.native import NativeSampler, pack_tape  # noqa: E402
+
+# three-parameter fixtures the single-chain replay covers (test_full_chain_replay), plus the
+# ragged no_outlier twin (n = 119 next to n = 130)
+REPLAY = [n for n in fixture_names()
+          if "fixed" in n and "vvh17" not in n and "efac" not in n]
+
+
+def _pad(a, nst):
+    out = np.zeros(a.shape[:-1] + (nst,))
+    out[..., :a.shape[-1]] = a
+    return out
+
+
+def test_batch_replays_every_fixture():
+    assert any(n.startswith("simclean") for n in REPLAY)
+    refs = [load_ref(n) for n in REPLAY]
+    ns = NativeSampler([r["pta"] for r in refs], [r["kw"] for r in refs], 0)
+    C = len(refs)
+    ns.alloc(C, dataset=np.arange(C))
+    nst = ns.n
+    assert nst == max(r["pta"].n for r in refs) and min(r["pta"].n for r in refs) < nst
+    S = int(refs[0]["niter"])
+    s0 = [sweep_state(r, 0) for r in refs]
+    ns.set_state(x=np.stack([r["xs"] for r in refs]), b=np.stack([s["b"] for s in s0]),
+                 z=np.stack([_pad(s["z"], nst) for s in s0]),
+                 alpha=np.stack([_pad(s["alpha"], nst) for s in s0]),
+                 pout=np.stack([_pad(s["pout"], nst) for s in s0]),
+                 theta=np.array([s["theta"] for s in s0]), nu=np.array([s["nu"] for s in s0]))
+    tape = np.stack([pack_tape(r["tape"], np.arange(S), r["pta"].n, ns.m, ns.stride, nst)
+                     for r in refs])
+    rec = ns.alloc_records(S)
+    for v in rec.values():
+        v.zero_()
+    ns.sweep(S, records=rec, tape=torch.as_tensor(tape).to(ns.tdev).contiguous())
+    got = {k: v.cpu().numpy() for k, v in rec.items()}
+    assert np.all(ns.get_state()["status"] == 0)
+    for c, (name, r) in enumerate(zip(REPLAY, refs)):
+        n = r["pta"].n
+        np.testing.assert_array_equal(got["x"][c], r["chain"], err_msg=name)
+        np.testing.assert_array_equal(got["z"][c][:, :n], r["zchain"], err_msg=name)
+        np.testing.assert_array_equal(got["nu"][c], r["dfchain"], err_msg=name)
+        for k, rk in (("b", "bchain"), ("alpha", "alphachain"), ("pout", "poutchain"),
+                      ("theta", "thetachain")):
+            g = got[k][c][..., :n] if k in ("alpha", "pout") else got[k][c]
+            rel = np.abs(g - r[rk]) / np.maximum(np.abs(r[rk]), 1e-300)
+            assert np.all(rel <= 1e-6), f"{name} {k}: max rel {rel.max():.3e}"
+        # TOAs beyond this dataset's n are never written
+        assert np.all(got["alpha"][c][:, n:] == 0.0) if n < nst else True
+
+
+def test_batch_equals_single_dataset_launches():
+    """Philox mode: chains in a ragged multi-model batch == their dataset launched alone."""
+    names = ["beta_fixed", "simclean_beta_fixed", "sim_t_fixed", "simclean_vvh17_fixed"]
+    refs = [load_ref(n) for n in names]
+    per, S, seed = 6, 7, 4242
+    C = per * len(refs)
+    ds = np.repeat(np.arange(len(refs)), per)
+    big = NativeSampler([r["pta"] for r in refs], [r["kw"] for r in refs], 0)
+    big.alloc(C, dataset=ds)
+    nst = big.n
+
+    def init(r, k, width):
+        s = sweep_state(r, 0)
+        return dict(x=np.tile(r["xs"], (k, 1)), b=np.tile(s["b"], (k, 1)),
+                    z=np.tile(_pad(s["z"], width), (k, 1)),
+                    alpha=np.tile(_pad(s["alpha"], width), (k, 1)),
+                    pout=np.tile(_pad(s["pout"], width), (k, 1)),
+                    theta=np.full(k, s["theta"]), nu=np.full(k, s["nu"]))
+
+    parts = [init(r, per, nst) for r in refs]
+    big.set_state(**{k: np.concatenate([p[k] for p in parts]) for k in parts[0]})
+    big.sweep(S, seed=seed, sweep0=3)
+    full = big.get_state()
+    assert np.all(full["status"] == 0)
+    for d, r in enumerate(refs):
+        one = NativeSampler(r["pta"], r["kw"], 0)
+        one.alloc(per)
+        one.set_state(**init(r, per, r["pta"].n))
+        one.sweep(S, seed=seed, sweep0=3, chain0=d * per)
+        o = one.get_state()
+        sl = slice(d * per, (d + 1) * per)
+        n = r["pta"].n
+        for k in ("x", "b", "theta", "nu"):
+            np.testing.assert_array_equal(full[k][sl], o[k], err_msg=f"{names[d]} {k}")
+        for k in ("z", "alpha", "pout"):
+            np.testing.assert_array_equal(full[k][sl][:, :n], o[k], err_msg=f"{names[d]} {k}")
+        one.close()
+    big.close()
+
+
+def test_bad_dataset_index_is_flagged():
+    r = load_ref("beta_fixed")
+    ns = NativeSampler([r["pta"], r["pta"]], [r["kw"], r["kw"]], 0)
+    with pytest.raises(ValueError):
+        ns.alloc(2, dataset=[0, 2])
+    ns.alloc(2, dataset=[0, 1])
+    s = sweep_state(r, 0)
+    ns.set_state(x=np.tile(r["xs"], (2, 1)), z=np.tile(s["z"], (2, 1)),
+                 alpha=np.tile(s["alpha"], (2, 1)), theta=np.full(2, 0.01), nu=np.full(2, 4.0))
+    ns.dataset.copy_(torch.tensor([0, 7], dtype=torch.int32, device=ns.tdev))
+    ns.sweep(2, seed=1)
+    st = ns.get_state()
+    assert st["status"][0] == 0 and st["status"][1] == 4
+    np.testing.assert_array_equal(st["x"][1], r["xs"])   # untouched
+    ns.close()

@@ -285,9 +285,27 @@ def dataset_arrays(pta, psr):
                 tm_weight=pta.tm_weight, names=np.array(pta.param_names))
 
 
+def simclean(niter=12):
+    """simulate_data.py's no_outlier twin (outlier TOAs deleted, simulate_data.py:35-37):
+    n < 130, so a batch with the outlier dataset is ragged."""
+    sim, clean = gdata.simulate_data(seed=7, theta=0.1)
+    pta5 = PTA(clean)
+    np.savez_compressed(os.path.join(OUTDIR, "simclean_dataset.npz"),
+                        **dataset_arrays(pta5, clean))
+    for name in ("beta", "vvh17"):
+        out = run_one(pta5, name, MODELS[name], seed=778, niter=niter, x0=[4.33, -14.0, -7.6])
+        out["model_kw"] = np.array(repr(MODELS[name]))
+        np.savez_compressed(os.path.join(OUTDIR, f"ref_simclean_{name}_fixed.npz"), **out)
+        print("simclean", name, "n", pta5.n, "cond:", np.nanmax(out["tape_b_cond"]),
+              file=sys.stderr)
+
+
 def main():
     os.makedirs(OUTDIR, exist_ok=True)
     niter = 12
+    if "--only-simclean" in sys.argv:
+        simclean(niter)
+        return
     psr = gdata.j1713(seed=1713, theta=0.05)
     pta = PTA(psr)
     np.savez_compressed(os.path.join(OUTDIR, "j1713_dataset.npz"), **dataset_arrays(pta, psr))
@@ -328,6 +346,7 @@ def main():
                   x0=[4.33, -14.0, -7.6])
     out["model_kw"] = np.array(repr(MODELS["uniform"]))
     np.savez_compressed(os.path.join(OUTDIR, "ref_twob_uniform_fixed.npz"), **out)
+    simclean(niter)
 
 
 if __name__ == "__main__":
