@@ -79,11 +79,13 @@ def design_matrix(mjd: np.ndarray, par: dict, fit: list) -> np.ndarray:
 
 
 def simulate_residuals(toas, toaerrs, U, *, theta=0.05, sigma_out=1e-6, log10_A=-14.0,
-                       gamma=4.33, components=30, rng=None, red=None):
+                       gamma=4.33, components=30, rng=None, red=None, dof=None):
     """One realisation of the simulate_data.py:10-39 recipe at given epochs.
 
     Returns ``(residuals, z)``: white + red + outliers with the timing model projected
-    out (``r - U U^T r``); ``z`` are the injected outlier flags.
+    out (``r - U U^T r``); ``z`` are the injected outlier flags.  ``dof`` (not in the
+    reference; the BASELINE config-4 Student-t grid) replaces the Gaussian white noise of
+    the non-outlier TOAs by sigma * t_dof draws.
     """
     rng = np.random.default_rng() if rng is None else rng
     n = len(toas)
@@ -92,7 +94,8 @@ def simulate_residuals(toas, toaerrs, U, *, theta=0.05, sigma_out=1e-6, log10_A=
         phi = powerlaw(ff, log10_A, gamma)
         red = F @ (np.sqrt(phi) * rng.standard_normal(2 * components))
     z = (rng.random(n) < theta).astype(np.int64)
-    r = red + ((1 - z) * toaerrs + z * sigma_out) * rng.standard_normal(n)
+    xi = rng.standard_normal(n) if dof is None else rng.standard_t(dof, n)
+    r = red + ((1 - z) * toaerrs + z * sigma_out) * xi
     r = r - U @ (U.T @ r)
     return r, z
 
@@ -121,7 +124,7 @@ def j1713(seed: int = 1713, theta: float = 0.05, sigma_out: float = 1e-6,
 
 
 def simulate_data(seed: int, theta: float = 0.05, sigma_out: float = 1e-6,
-                  red_source: str = "powerlaw"):
+                  red_source: str = "powerlaw", dof=None):
     """Restatement of simulate_data.py:10-39 on the J1713+0747 epochs.
 
     Error bars are log-normal ``10^(-7 + 0.2 xi)`` s (simulate_data.py:15).  Returns the
@@ -137,7 +140,7 @@ def simulate_data(seed: int, theta: float = 0.05, sigma_out: float = 1e-6,
     U = np.linalg.svd(M, full_matrices=False)[0]
     red = raw["red"] * DAY_SEC if red_source == "red.txt" else None
     r, z = simulate_residuals(toas, err, U, theta=theta, sigma_out=sigma_out, rng=rng,
-                              red=red)
+                              red=red, dof=dof)
     out = PulsarData(name="J1713+0747", toas=toas, residuals=r, toaerrs=err, Mmat=M,
                      meta={"z_true": z, "seed": seed, "theta": theta})
     keep = z == 0
