@@ -1,6 +1,6 @@
 """Benchmark: aggregate Gibbs sweeps/s (+ ESS/s) on J1713+0747, batched chains per GPU.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--chains C]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--chains C] [--config 2|3|4]
 
 A *step* is one Gibbs sweep (gibbs.py:354-380) of every chain on every rank.  Each rank
 owns C chains (weak scaling, default 1024 = BASELINE config 2 per GPU) of the run_sims.py
@@ -100,12 +100,71 @@ def initial_state(pta, C: int, chain0: int):
                 pout=np.zeros((C, n)), theta=np.full(C, 0.01), nu=np.full(C, 4.0))
 
 
+def workload(config: int, rank: int, world: int, chains: int | None):
+    """BASELINE.json configs as (datasets, cfgs, chain->dataset, initial state, description).
+
+    2: J1713+0747 epochs, 1024 chains per GPU (the headline, default);
+    3: simulate_data.py pulsar, 5% outliers, red.txt red noise, 512 chains per GPU
+       (4096 over 8 GPUs);
+    4: run_sims.py grid, 256 datasets (3 outlier fractions x {Gaussian, Student-t nu=4}
+       white noise x outlier/no_outlier twins x 5 outlier models) x 64 chains, 32
+       datasets per GPU.
+    All weak scaling: the per-GPU work is fixed as the GPU count grows.
+    """
+    from gibbs_student_t_amd import data
+    from gibbs_student_t_amd import run_sims
+    from gibbs_student_t_amd.model import PTA
+    if config in (2, 3):
+        if config == 2:
+            pta = PTA(data.j1713())
+            C = chains or 1024
+            desc = ("J1713+0747 Student-t/outlier-mixture Gibbs sampler (run_sims 'beta' "
+                    "model), fp64")
+            dat = ("synthetic residuals at the 130 real J1713+0747 TOA epochs (white + "
+                   "power-law red + 5% outliers, seeded); chains start from prior draws")
+        else:
+            out, _ = data.simulate_data(seed=2017, theta=0.05, red_source="red.txt")
+            pta = PTA(out)
+            C = chains or 512
+            desc = ("simulate_data.py pulsar (J1713+0747 epochs, log-normal errors, red.txt "
+                    "red noise, 5% outliers), run_sims 'beta' model, fp64")
+            dat = ("simulate_data.py restatement: log-normal error bars, the reference's "
+                   "red.txt realisation, Bernoulli(0.05) outliers with sigma_out = 1 us")
+        c0 = rank * C
+        return dict(ptas=[pta], cfgs=[CFG], ds=np.zeros(C, np.int32),
+                    init=initial_state(pta, C, c0), chain0=c0, C=C, desc=desc, data=dat,
+                    per=C)
+    if config == 4:
+        per_entry = chains or 64
+        grid = run_sims.build_grid(thetas=(0.05, 0.1, 0.15), realisations=5,
+                                   dofs=(None, 4.0))[:256]
+        per_rank = 256 // 8 if world <= 8 else max(1, 256 // world)
+        e0 = rank * per_rank
+        mine = grid[e0:e0 + per_rank]
+        nst = max(e.pta.n for e in mine)
+        parts = [run_sims.initial_state(e, per_entry, (e0 + i) * per_entry, 7, nst)
+                 for i, e in enumerate(mine)]
+        init = {k: np.concatenate([p_[k] for p_ in parts]) for k in parts[0]}
+        C = len(mine) * per_entry
+        return dict(ptas=[e.pta for e in mine], cfgs=[e.cfg for e in mine],
+                    ds=np.repeat(np.arange(len(mine)), per_entry).astype(np.int32), init=init,
+                    chain0=e0 * per_entry, C=C, per=per_entry,
+                    desc=("run_sims.py grid: 256 simulated datasets (theta 0.05/0.1/0.15, "
+                          "Gaussian and Student-t nu=4 white noise, outlier + no_outlier "
+                          "twins, 5 outlier models) x 64 chains, 32 datasets per GPU, fp64"),
+                    data="simulate_data.py restatement per dataset (seeded), ragged n")
+    raise SystemExit(f"unknown --config {config}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=300)
-    ap.add_argument("--chains", type=int, default=1024, help="chains per GPU")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4),
+                    help="BASELINE.json config (2 = headline J1713+0747, 1024 chains/GPU)")
+    ap.add_argument("--chains", type=int, default=None,
+                    help="chains per GPU (config 4: per dataset)")
     ap.add_argument("--seed", type=int, default=20171713)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -123,20 +182,18 @@ def main():
         cpu = cpu_baseline(args.cpu_seconds, cores)      # before the GPU is touched
 
     import torch
-    from gibbs_student_t_amd import data, diag
-    from gibbs_student_t_amd.model import PTA
+    from gibbs_student_t_amd import diag
     from gibbs_student_t_amd.native import NativeSampler
 
     rank, local, world = dist.init()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    pta = PTA(data.j1713())
-    n, m = pta.T.shape
-    C, K, W = args.chains, args.steps, args.warmup
-    c0, _ = dist.chain_range(rank, C)
-    ns = NativeSampler(pta, CFG, local)
-    ns.alloc(C)
-    ns.set_state(**initial_state(pta, C, c0))
+    wl = workload(args.config, rank, world, args.chains)
+    C, K, W = wl["C"], args.steps, args.warmup
+    c0 = wl["chain0"]
+    ns = NativeSampler(wl["ptas"], wl["cfgs"], local)
+    ns.alloc(C, dataset=wl["ds"])
+    ns.set_state(**wl["init"])
     if W > 0:
         ns.sweep(W, seed=args.seed, sweep0=0, chain0=c0)
     rec = ns.alloc_records(K)
@@ -152,15 +209,24 @@ def main():
     kernel_ms = ns.last_kernel_ms()
     status = ns.get_state()["status"]
 
-    # ESS over this rank's chains, then summed over ranks (disjoint chain sets)
+    # ESS per dataset (its chains share one posterior), summed over datasets and ranks
     xs = rec["x"].cpu().numpy()
     th = rec["theta"].cpu().numpy()
-    names = [p.name.split("_", 1)[1] for p in pta.params]
-    series = {nm: xs[:, :, j] for j, nm in enumerate(names)}
-    series["theta"] = th
-    ess = {k: diag.bulk_ess(v) for k, v in series.items()}
-    rhat = {k: diag.split_rhat(v) for k, v in series.items()}
-    keys = list(series)
+    names = [p.name.split("_", 1)[1] for p in wl["ptas"][0].params]
+    keys = names + ["theta"]
+    ess = {k: 0.0 for k in keys}
+    rhat = {k: 0.0 for k in keys}
+    for d in range(len(wl["ptas"])):
+        sel = wl["ds"] == d
+        series = {nm: xs[sel, :, j] for j, nm in enumerate(names)}
+        series["theta"] = th[sel]
+        for k, v in series.items():
+            if k == "theta" and wl["cfgs"][d]["model"] not in ("mixture", "vvh17"):
+                continue            # theta is never updated: no ESS to speak of
+            e = diag.bulk_ess(v)
+            ess[k] += e if np.isfinite(e) else 0.0
+            r = diag.split_rhat(v)
+            rhat[k] = max(rhat[k], r if np.isfinite(r) else 0.0)
     s_vec = np.array([ess[k] for k in keys] + [float((status != 0).sum())])
     m_vec = np.array([elapsed, kernel_ms] + [rhat[k] for k in keys])
     s_vec, m_vec = dist.reduce_summary(s_vec, m_vec, dev)
@@ -171,17 +237,20 @@ def main():
     if rank == 0:
         total = C * world * K
         value = total / elapsed
-        flops = algorithmic_flops(n, m) * C * K
+        n_mean = float(np.mean([p_.T.shape[0] for p_ in wl["ptas"]]))
+        n, m = wl["ptas"][0].T.shape
+        n_eff = n if args.config != 4 else n_mean
+        flops = algorithmic_flops(n_eff, m) * C * K
         achieved = flops / (kernel_ms * 1e-3) / 1e12
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
+        if os.path.exists(pmc) and args.config == 2:
             try:
                 pj = json.load(open(pmc))
                 traffic = pj["hbm_bytes_per_chain_sweep"] * C * K
             except Exception:
                 traffic = None
-        min_ess = float(min(ess_tot.values()))
+        min_ess = float(min(v for v in ess_tot.values() if v > 0))
         out = {
             "metric": METRIC,
             "value": value,
@@ -194,13 +263,11 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic residuals at the 130 real J1713+0747 TOA epochs "
-                    "(white + power-law red + 5% outliers, seeded); chains start from prior "
-                    "draws",
-            "config": {"workload": "J1713+0747 Student-t/outlier-mixture Gibbs sampler "
-                                   "(run_sims 'beta' model), fp64",
+            "data": wl["data"],
+            "config": {"workload": wl["desc"], "baseline_config": args.config,
                        "chains_per_gpu": C, "chains_total": C * world, "n_toa": n,
-                       "basis_cols": m, "record_every": 1,
+                       "basis_cols": m, "datasets_per_gpu": len(wl["ptas"]),
+                       "record_every": 1,
                        "parallelism": f"independent chains sharded over {world} GPU(s); "
                                       "RCCL only for the final summary all-reduce"},
             "ess_per_sec": min_ess / elapsed,
@@ -211,8 +278,8 @@ def main():
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
                          "traffic": traffic,
-                         "algorithmic_flop_per_chain_sweep": algorithmic_flops(n, m),
-                         "toa_pass_GBps": toa_pass_bytes(n) * C * K / (kernel_ms * 1e-3)
+                         "algorithmic_flop_per_chain_sweep": algorithmic_flops(n_eff, m),
+                         "toa_pass_GBps": toa_pass_bytes(n_eff) * C * K / (kernel_ms * 1e-3)
                          / 1e9},
             "cpu_baseline": cpu,
         }
