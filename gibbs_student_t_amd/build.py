@@ -9,7 +9,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libgst.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("gst.hip", "gst_kernel.hpp", "philox.hpp")]
+SOURCES = [os.path.join(CSRC, f) for f in ("gst.hip", "gst_kernel.hpp", "gst_large.hpp",
+                                            "philox.hpp")]
 HEADER = os.path.join(ROOT, "include", "gst.h")
 
 

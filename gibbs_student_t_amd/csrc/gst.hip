@@ -14,6 +14,7 @@
 
 #include "gst.h"
 #include "gst_kernel.hpp"
+#include "gst_large.hpp"
 
 namespace {
 
@@ -38,10 +39,27 @@ struct Ctx {
   gst::DevModel* dmd = nullptr;    // device array [nd] (in allocs)
   int nd = 0, nmax = 0, m = 0, raug = 0;
   int MT = 0, NS = 0, K0 = 0, WPB = 4;
+  int path_req = GST_PATH_AUTO;    // gst_set_path
+  int path = GST_PATH_PERSISTENT;  // chosen by gst_model_set
   std::vector<void*> allocs;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
+  // large path: scratch sized for scratch_C chains, per-kernel timing events
+  gst::LScratch ls{};
+  int scratch_C = 0;
+  size_t lds_tm = 0, lds_hyper = 0, lds_btm = 0;
+  bool timing = false;
+  std::vector<hipEvent_t> evpool;
+  std::vector<int> evkind;  // kind of event pair i (events 2i, 2i+1)
+  size_t evused = 0;
 };
+
+void free_scratch(Ctx* cx) {
+  for (double* p : {cx->ls.G, cx->ls.y, cx->ls.w, cx->ls.sc, cx->ls.v})
+    if (p) (void)hipFree(p);
+  cx->ls = gst::LScratch{};
+  cx->scratch_C = 0;
+}
 
 int upload(Ctx* cx, const void* host, size_t bytes, void** dev) {
   void* p = nullptr;
@@ -59,6 +77,7 @@ void free_model(Ctx* cx) {
   cx->dmd = nullptr;
   cx->nd = 0;
   cx->has_model = false;
+  free_scratch(cx);
 }
 
 typedef void (*kfn_t)(const gst::DevModel*, const gst::DevState, const gst::DevRec,
@@ -118,6 +137,7 @@ int gst_ctx_destroy(void* ctx) {
   if (!cx) return 0;
   (void)hipSetDevice(cx->device);
   free_model(cx);
+  for (hipEvent_t e : cx->evpool) (void)hipEventDestroy(e);
   if (cx->ev0) (void)hipEventDestroy(cx->ev0);
   if (cx->ev1) (void)hipEventDestroy(cx->ev1);
   delete cx;
@@ -125,9 +145,9 @@ int gst_ctx_destroy(void* ctx) {
 }
 
 // Pack one dataset's constants (shapes already validated) into device buffers owned by cx.
-static int pack_dataset(Ctx* cx, const gst_model_desc* d, gst::DevModel& md) {
+static int pack_dataset(Ctx* cx, const gst_model_desc* d, gst::DevModel& md, int tm_align) {
   const int n = d->n, m = d->m, nf = d->nfourier, ntm = d->ntm, P = d->nparams;
-  const int ntm_pad = round_up(ntm > 0 ? ntm : 1, 8);
+  const int ntm_pad = round_up(ntm > 0 ? ntm : 1, tm_align);
   const int raug = ntm_pad + nf;
   const int mpad = round_up(raug + 1, 16);
   const int npad = 64 * ((n + 63) / 64);
@@ -232,6 +252,7 @@ static int pack_dataset(Ctx* cx, const gst_model_desc* d, gst::DevModel& md) {
 
   md.n = n;
   md.m = m;
+  md.mp = mpad;
   md.nf = nf;
   md.ntm = ntm;
   md.ntm_pad = ntm_pad;
@@ -336,19 +357,28 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
   const int MT = mpad / 8, K0 = ntm_pad / 8;
   const int nsl = (nmax + 63) / 64;
   const int NS = nsl <= 2 ? 2 : (nsl <= 3 ? 3 : 4);
-  if (round_up(nmax, 4) > 64 * NS) return fail("gst_model_set: n too large for TOA slots");
-  if (!pick(MT, NS, K0, raug, false)) {
-    char b[200];
+  const bool fits = round_up(nmax, 4) <= 64 * NS && pick(MT, NS, K0, raug, false);
+  int path = cx->path_req;
+  if (path == GST_PATH_AUTO) path = fits ? GST_PATH_PERSISTENT : GST_PATH_LARGE;
+  if (path == GST_PATH_PERSISTENT && !fits) {
+    char b[220];
     std::snprintf(b, sizeof b,
-                  "gst_model_set: no kernel instance for MT=%d NS=%d K0=%d RA=%d (n=%d m=%d "
-                  "nfourier=%d ntm=%d); add a GST_CASE in gst.hip",
-                  MT, NS, K0, raug, nmax, m, nf, ntm);
+                  "gst_model_set: no persistent-kernel instance for MT=%d NS=%d K0=%d RA=%d "
+                  "(n=%d m=%d nfourier=%d ntm=%d); use the large path", MT, NS, K0, raug,
+                  nmax, m, nf, ntm);
     return fail(b);
   }
+  if (path == GST_PATH_LARGE) {
+    if (nd != 1) return fail("gst_model_set: the large path takes one dataset per context");
+    const int ms = nf + 1;
+    if ((size_t)(ms * (ms + 1) + nf + 2 * ms) * 8 > 160 * 1024)
+      return fail("gst_model_set: large path needs nfourier <= 138 (LDS-resident Fourier block)");
+  }
   free_model(cx);
+  const int tm_align = path == GST_PATH_LARGE ? 16 : 8;
   std::vector<gst::DevModel> hmd(nd);
   for (int i = 0; i < nd; ++i)
-    if (pack_dataset(cx, &descs[i], hmd[i])) {
+    if (pack_dataset(cx, &descs[i], hmd[i], tm_align)) {
       free_model(cx);
       return -1;
     }
@@ -364,6 +394,21 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
   cx->raug = raug;
   cx->m = m;
   cx->WPB = gst::wpb_for(MT, NS);
+  cx->path = path;
+  if (path == GST_PATH_LARGE) {
+    const gst::DevModel& h = hmd[0];
+    cx->raug = h.raug;
+    cx->lds_tm = (size_t)h.mp * (gst::TM_PW + 1) * 8;
+    const int ms = h.nf + 1;
+    cx->lds_hyper = (size_t)(ms * (ms + 1) + h.nf + 2 * ms) * 8;
+    cx->lds_btm = (size_t)(3 * h.ntm_pad + h.raug) * 8;
+    HIP_OK(hipFuncSetAttribute((const void*)gst::lg_tmelim,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)cx->lds_tm));
+    HIP_OK(hipFuncSetAttribute((const void*)gst::lg_hyper,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)cx->lds_hyper));
+    HIP_OK(hipFuncSetAttribute((const void*)gst::lg_btm,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)cx->lds_btm));
+  }
   cx->has_model = true;
   return 0;
 }
@@ -379,6 +424,95 @@ int gst_model_info(void* ctx, int* ndatasets, int* nmax, int* tape_stride) {
   return 0;
 }
 
+// timing events (gst_set_timing): pair i brackets one launch of kernel kind evkind[i]
+static int ev_mark(Ctx* cx, int kind, hipStream_t st, bool begin) {
+  if (!cx->timing) return 0;
+  if (begin) {
+    if (2 * cx->evused + 2 > cx->evpool.size()) {
+      hipEvent_t e0, e1;
+      HIP_OK(hipEventCreate(&e0));
+      HIP_OK(hipEventCreate(&e1));
+      cx->evpool.push_back(e0);
+      cx->evpool.push_back(e1);
+      cx->evkind.push_back(0);
+    }
+    cx->evkind[cx->evused] = kind;
+    HIP_OK(hipEventRecord(cx->evpool[2 * cx->evused], st));
+  } else {
+    HIP_OK(hipEventRecord(cx->evpool[2 * cx->evused + 1], st));
+    ++cx->evused;
+  }
+  return 0;
+}
+
+#define LG_LAUNCH(kind, kern, grid, block, lds)                                  \
+  do {                                                                           \
+    if (ev_mark(cx, kind, st, true)) return -1;                                  \
+    hipLaunchKernelGGL(kern, grid, block, lds, st, cx->dmd, a);                  \
+    HIP_OK(hipGetLastError());                                                   \
+    if (ev_mark(cx, kind, st, false)) return -1;                                 \
+  } while (0)
+
+static int ensure_scratch(Ctx* cx, int C) {
+  if (C <= cx->scratch_C) return 0;
+  free_scratch(cx);
+  const gst::DevModel& h = cx->hmd[0];
+  const size_t mp = h.mp, npad = h.npad;
+  HIP_OK(hipMalloc(&cx->ls.G, (size_t)C * mp * mp * 8));
+  HIP_OK(hipMalloc(&cx->ls.y, (size_t)C * npad * 8));
+  HIP_OK(hipMalloc(&cx->ls.w, (size_t)C * npad * 8));
+  HIP_OK(hipMalloc(&cx->ls.sc, (size_t)C * 16 * 8));
+  HIP_OK(hipMalloc(&cx->ls.v, (size_t)C * mp * 8));
+  HIP_OK(hipMemset(cx->ls.G, 0, (size_t)C * mp * mp * 8));
+  HIP_OK(hipMemset(cx->ls.v, 0, (size_t)C * mp * 8));
+  cx->scratch_C = C;
+  return 0;
+}
+
+// One sweep = record, white, gram, tmelim, hyper, btm, tb, toa launches (gst_large.hpp).
+static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
+                        const gst::DevTape& dt, int C, int nsweeps, long long sweep0,
+                        int record_every, unsigned mask, unsigned long long seed,
+                        long long chain0, int eval_only, double* ow, double* oh,
+                        hipStream_t st) {
+  if (ensure_scratch(cx, C)) return -1;
+  const gst::DevModel& h = cx->hmd[0];
+  gst::LArgs a{ds, dr, dt, cx->ls, C, nsweeps, 0, record_every, mask, seed, sweep0, chain0,
+               eval_only, ow, oh};
+  const int nsb = (h.mp / 16 + 3) / 4;
+  const int npairs = nsb * (nsb + 1) / 2;
+  const dim3 g_chain(C), b_chain(gst::LBLK);
+  const dim3 g_gram(npairs * ((C + gst::GRAM_WAVES - 1) / gst::GRAM_WAVES)), b_gram(64 * gst::GRAM_WAVES);
+  const dim3 g_tb(h.npad / 64, (C + 63) / 64);
+  cx->evused = 0;
+  HIP_OK(hipEventRecord(cx->ev0, st));
+  LG_LAUNCH(GST_K_TB, gst::lg_tb, g_tb, b_chain, 0);   // y = r - T b for the current b
+  const bool rec_on = record_every > 0 && !eval_only;
+  const int nit = eval_only ? 1 : nsweeps;
+  for (int it = 0; it < nit; ++it) {
+    a.it = it;
+    if (rec_on && it % record_every == 0) LG_LAUNCH(GST_K_RECORD, gst::lg_record, g_chain, b_chain, 0);
+    LG_LAUNCH(GST_K_WHITE, gst::lg_white, g_chain, b_chain, 0);
+    if ((mask & 6u) || eval_only) {
+      if (ev_mark(cx, GST_K_GRAM, st, true)) return -1;
+      hipLaunchKernelGGL(gst::lg_gram, g_gram, b_gram, 0, st, cx->dmd, a, nsb, npairs);
+      HIP_OK(hipGetLastError());
+      if (ev_mark(cx, GST_K_GRAM, st, false)) return -1;
+      LG_LAUNCH(GST_K_TMELIM, gst::lg_tmelim, g_chain, b_chain, cx->lds_tm);
+      LG_LAUNCH(GST_K_HYPER, gst::lg_hyper, g_chain, b_chain, cx->lds_hyper);
+      if (eval_only) break;
+      if (mask & 4u) {
+        LG_LAUNCH(GST_K_BTM, gst::lg_btm, g_chain, b_chain, cx->lds_btm);
+        LG_LAUNCH(GST_K_TB, gst::lg_tb, g_tb, b_chain, 0);
+      }
+    }
+    if (!eval_only && (mask & 0x78u)) LG_LAUNCH(GST_K_TOA, gst::lg_toa, g_chain, b_chain, 0);
+  }
+  HIP_OK(hipEventRecord(cx->ev1, st));
+  cx->timed = true;
+  return 0;
+}
+
 static int launch(Ctx* cx, const gst_state* s, const gst_records* r, const gst_tape* tp,
                   int C, int nsweeps, long long sweep0, int record_every, unsigned mask,
                   unsigned long long seed, long long chain0, int eval_only, double* ow,
@@ -389,8 +523,6 @@ static int launch(Ctx* cx, const gst_state* s, const gst_records* r, const gst_t
   if (C <= 0) return 0;
   HIP_OK(hipSetDevice(cx->device));
   const bool tape = tp && tp->data;
-  kfn_t k = pick(cx->MT, cx->NS, cx->K0, cx->raug, tape);
-  if (!k) return fail("gst: no kernel instance");
   if (!s->dataset && cx->nd > 1)
     return fail("gst: the model has several datasets: state.dataset must be set");
   gst::DevState ds{s->x,     s->b,  s->z,      s->alpha,  s->pout,
@@ -401,6 +533,11 @@ static int launch(Ctx* cx, const gst_state* s, const gst_records* r, const gst_t
   if (tape && tp->stride != gst_tape_stride(cx->nmax, cx->m))
     return fail("gst: tape stride mismatch");
   gst::DevTape dt{tape ? tp->data : nullptr, tape ? tp->stride : 0};
+  if (cx->path == GST_PATH_LARGE)
+    return launch_large(cx, ds, dr, dt, C, nsweeps, sweep0, record_every, mask, seed, chain0,
+                        eval_only, ow, oh, (hipStream_t)stream);
+  kfn_t k = pick(cx->MT, cx->NS, cx->K0, cx->raug, tape);
+  if (!k) return fail("gst: no kernel instance");
   const dim3 grid((C + cx->WPB - 1) / cx->WPB), block(64 * cx->WPB);
   hipStream_t st = (hipStream_t)stream;
   HIP_OK(hipEventRecord(cx->ev0, st));
@@ -447,6 +584,48 @@ int gst_sync(void* ctx, void* stream) {
   Ctx* cx = static_cast<Ctx*>(ctx);
   if (cx) HIP_OK(hipSetDevice(cx->device));
   HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+  return 0;
+}
+
+int gst_set_path(void* ctx, int path) {
+  Ctx* cx = static_cast<Ctx*>(ctx);
+  if (!cx) return fail("gst_set_path: null ctx");
+  if (path < GST_PATH_AUTO || path > GST_PATH_LARGE) return fail("gst_set_path: bad path");
+  cx->path_req = path;
+  return 0;
+}
+
+int gst_get_path(void* ctx, int* path) {
+  Ctx* cx = static_cast<Ctx*>(ctx);
+  if (!cx || !path) return fail("gst_get_path: null argument");
+  if (!cx->has_model) return fail("gst_get_path: no model set");
+  *path = cx->path;
+  return 0;
+}
+
+int gst_set_timing(void* ctx, int on) {
+  Ctx* cx = static_cast<Ctx*>(ctx);
+  if (!cx) return fail("gst_set_timing: null ctx");
+  cx->timing = on != 0;
+  return 0;
+}
+
+int gst_kernel_times(void* ctx, double* ms, int* launches, int nkinds) {
+  Ctx* cx = static_cast<Ctx*>(ctx);
+  if (!cx || !ms || !launches) return fail("gst_kernel_times: null argument");
+  for (int k = 0; k < nkinds; ++k) {
+    ms[k] = 0.0;
+    launches[k] = 0;
+  }
+  for (size_t i = 0; i < cx->evused; ++i) {
+    const int k = cx->evkind[i];
+    if (k < 0 || k >= nkinds) continue;
+    HIP_OK(hipEventSynchronize(cx->evpool[2 * i + 1]));
+    float f = 0.f;
+    HIP_OK(hipEventElapsedTime(&f, cx->evpool[2 * i], cx->evpool[2 * i + 1]));
+    ms[k] += f;
+    launches[k] += 1;
+  }
   return 0;
 }
 

@@ -56,7 +56,7 @@ struct DevModel {
   const double* csig2;   // [ncls]  sigma^2 of each class
   const double* ccount;  // [ncls]  TOAs per class
   int ncls;              // 0 = per-TOA white likelihood; 1..8 = class path
-  int n, m, nf, ntm, ntm_pad, raug, nks, npad, nslot_toa;
+  int n, m, mp, nf, ntm, ntm_pad, raug, nks, npad, nslot_toa;
   int P;
   int idx_efac, idx_equad, idx_logA, idx_gamma;
   double efac_const;

@@ -1,0 +1,846 @@
+// Large-model path (BASELINE config 5: n ~ 1e5 TOAs, m ~ 420 basis columns) for gfx950.
+//
+// The register-resident persistent kernel (gst_kernel.hpp) holds a whole chain in one
+// wavefront; that stops at m ~ 80 and n ~ 256.  Here one sweep of every chain is a short
+// pipeline of launches on one stream, each kernel shaped for its own roofline:
+//
+//   record   state -> chain records (gibbs.py:355-361)                       HBM copy
+//   white    21 white-noise likelihoods + MH (gibbs.py:114-143, 262-284),
+//            then N^-1, sum log N, r^T N^-1 r at the final white x            HBM/VALU
+//   gram     G_c = [T|r]^T diag(N_c^-1) [T|r] for every chain c               fp64 MFMA
+//            (gibbs.py:302-304): T HBM-resident and shared by all chains; one
+//            workgroup = 8 chains x one 64x64 super-tile, full TOA range
+//   tmelim   timing-model columns eliminated once per sweep (blocked right-    fp64 MFMA
+//            looking LDL^T, 16-column panels in LDS, MFMA trailing update)
+//            -> Schur complement S0 of the Fourier block + augmented row
+//   hyper    10 red-noise MH steps (gibbs.py:80-111, 288-329): S0 + diag(phi^-1)
+//            factored in LDS per proposal; b draw's Fourier part (gibbs.py:145-182)
+//   btm      b draw's timing-model part (back substitution through G)
+//   tb       y = r - T b for all chains as one MFMA GEMM (T streamed once)    fp64 MFMA
+//   toa      theta, z, alpha, nu (gibbs.py:185-259)                           HBM/VALU
+//
+// Variates use the same Philox counters as the persistent kernel (stage tags, step and
+// TOA indices), so both paths draw identical numbers for the same (seed, chain, sweep).
+// Internal column order as in gst_kernel.hpp, [TM | pad | Fourier | r | pad], with the
+// TM block padded to a multiple of 16 (one MFMA tile) and the dimension mp to 16.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "gst_kernel.hpp"
+
+namespace gst {
+
+constexpr int LBLK = 256;      // threads of the per-chain kernels (4 waves)
+constexpr int GRAM_WAVES = 8;  // chains per gram workgroup
+constexpr int TM_PW = 16;      // panel width of the timing-model elimination
+
+struct LScratch {
+  double* G;   // [C][mp*mp] Gram / factor (row-major, lower triangle)
+  double* y;   // [C][npad]  r - T b
+  double* w;   // [C][npad]  1/N (white scratch: y^2/a during the white block)
+  double* sc;  // [C][16]    per-chain scalars (SC_*)
+  double* v;   // [C][mp]    b-draw solution (internal order)
+};
+enum : int {
+  SC_LOGDETN = 0,
+  SC_RNR = 1,
+  SC_LDTM = 2,
+  SC_QUADTM = 3,
+  SC_FAILTM = 4,
+  SC_XLAST = 5,
+  SC_REDRAW = 6,
+  SC_FB = 7,
+};
+
+struct LArgs {
+  DevState st;
+  DevRec rec;
+  DevTape tape;
+  LScratch s;
+  int C, nsweeps, it, record_every;
+  unsigned mask;
+  unsigned long long seed;
+  long long sweep0, chain0;
+  int eval_only;
+  double *out_w, *out_h;
+};
+
+__device__ __forceinline__ Rng make_rng(const LArgs& a, int c) {
+  Rng r;
+  r.k0 = (uint32_t)(a.seed & 0xffffffffull);
+  r.k1 = (uint32_t)(a.seed >> 32);
+  r.chain = (uint32_t)(a.chain0 + c);
+  r.sweep = (uint32_t)(a.sweep0 + a.it);
+  return r;
+}
+
+__device__ __forceinline__ const double* tape_row(const LArgs& a, int c) {
+  return a.tape.data ? a.tape.data + ((size_t)c * a.nsweeps + a.it) * a.tape.stride : nullptr;
+}
+
+// Deterministic block sum (4 waves): every thread gets the bitwise-identical value.
+__device__ __forceinline__ double block_sum(double v, double* red) {
+  v = wave_sum(v);
+  const int wv = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[wv] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// MH variates of global step gs (0..19 white, 20..29 hyper) exactly as the persistent
+// kernel draws them (gst_kernel.hpp mh_variates): parameter, jump, log(u_acc), 10^(2 jump).
+__device__ __forceinline__ void mh_variate(const DevModel& md, const Rng& rng, const double* tp,
+                                           int gs, double* out4) {
+  const bool white = gs < NWHITE;
+  const int step = white ? gs : gs - NWHITE;
+  double us, par, xi, la;
+  if (tp) {
+    const double* e = tp + (white ? TP_WHITE : TP_HYPER) + 4 * step;
+    us = e[0];
+    par = e[1];
+    xi = e[2];
+    la = log(e[3]);
+  } else {
+    const uint32_t tag = white ? TAG_WHITE : TAG_HYPER;
+    double ua, ub, uidx, unused;
+    rng.uniform2(0u, tag | (uint32_t)(3 * step), ua, ub);
+    us = ua;
+    la = log(ub);
+    xi = normal_from(rng, 0u, tag | (uint32_t)(3 * step + 1));
+    const int nind = white ? md.nw : md.nh;
+    rng.uniform2(0u, tag | (uint32_t)(3 * step + 2), uidx, unused);
+    int k = (int)(uidx * nind);
+    k = k < nind - 1 ? k : nind - 1;
+    par = (double)(white ? iget4(md.wind, k) : iget4(md.hind, k));
+  }
+  int cnt = 0;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) cnt += (md.mh_cdf[i] <= us) ? 1 : 0;
+  cnt = cnt < 4 ? cnt : 4;
+  const double scale = md.mh_size[0] * (cnt == 0) + md.mh_size[1] * (cnt == 1) +
+                       md.mh_size[2] * (cnt == 2) + md.mh_size[3] * (cnt == 3) +
+                       md.mh_size[4] * (cnt == 4);
+  const double delta = mh_step(xi, white ? md.sig_w : md.sig_h, scale);
+  out4[0] = par;
+  out4[1] = delta;
+  out4[2] = la;
+  out4[3] = exp(2.0 * delta * 2.302585092994045684);
+}
+
+__device__ __forceinline__ double lnprior4(const DevModel& md, const double (&xq)[4]) {
+  bool in = true;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (j < md.P) in = in && (xq[j] >= md.pmin[j]) && (xq[j] <= md.pmax[j]);
+  return in ? md.lp_sum : -INFINITY;
+}
+
+__device__ __forceinline__ void load_x(const DevModel& md, const DevState& st, int c,
+                                       double (&x)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) x[j] = j < md.P ? st.x[(size_t)c * md.P + j] : 0.0;
+}
+
+// ------------------------------------------------------------------------------------
+// record: the state at the start of the sweep (gibbs.py:355-361)
+// ------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(LBLK) lg_record(const DevModel* __restrict__ mds, LArgs a) {
+  const int c = blockIdx.x;
+  const DevModel& md = mds[0];
+  const int ri = a.it / a.record_every;
+  if (ri >= a.rec.nrec) return;
+  const size_t base = (size_t)c * a.rec.nrec + ri;
+  const int n = md.n, m = md.m, nst = a.st.nst;
+  for (int j = threadIdx.x; j < md.P; j += LBLK)
+    if (a.rec.x) a.rec.x[base * md.P + j] = a.st.x[(size_t)c * md.P + j];
+  for (int j = threadIdx.x; j < m; j += LBLK)
+    if (a.rec.b) a.rec.b[base * m + j] = a.st.b[(size_t)c * m + j];
+  for (int t = threadIdx.x; t < n; t += LBLK) {
+    if (a.rec.z) a.rec.z[base * nst + t] = a.st.z[(size_t)c * nst + t];
+    if (a.rec.alpha) a.rec.alpha[base * nst + t] = a.st.alpha[(size_t)c * nst + t];
+    if (a.rec.pout) a.rec.pout[base * nst + t] = a.st.pout[(size_t)c * nst + t];
+  }
+  if (threadIdx.x == 0) {
+    if (a.rec.theta) a.rec.theta[base] = a.st.theta[c];
+    if (a.rec.nu) a.rec.nu[base] = a.st.nu[c];
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// white: MH over the white-noise parameters, then N^-1 for the Gram
+// ------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(LBLK) lg_white(const DevModel* __restrict__ mds, LArgs a) {
+  const int c = blockIdx.x;
+  const DevModel& md = mds[0];
+  __shared__ double red[4];
+  __shared__ double mhv[NWHITE][4];
+  const int n = md.n, nst = a.st.nst, npad = md.npad;
+  const double* zc = a.st.z + (size_t)c * nst;
+  const double* alc = a.st.alpha + (size_t)c * nst;
+  const double* yc = a.s.y + (size_t)c * npad;
+  double* wc = a.s.w + (size_t)c * npad;
+  double* sc = a.s.sc + (size_t)c * 16;
+  double xv[4];
+  load_x(md, a.st, c, xv);
+  if (threadIdx.x == 0) sc[SC_XLAST] = xv[md.P - 1];   // chain[ii, -1] (gibbs.py:373)
+  const Rng rng = make_rng(a, c);
+  const double* tp = tape_row(a, c);
+  const bool do_white = (a.mask & 1u) || a.eval_only;
+
+  if (do_white) {
+    // fixed over the block: a_t = alpha_t^z_t, y_t^2 / a_t and sum log a_t
+    double la = 0.0;
+    for (int t = threadIdx.x; t < n; t += LBLK) {
+      const bool zt = zc[t] != 0.0;
+      const double at = zt ? alc[t] : 1.0;
+      if (zt) la += log(at);
+      wc[t] = yc[t] * yc[t] / at;
+    }
+    la = block_sum(la, red);
+    if (!a.eval_only && threadIdx.x < NWHITE) mh_variate(md, rng, tp, threadIdx.x, mhv[threadIdx.x]);
+    __syncthreads();
+    auto lnl = [&](const double (&q)[4], double Q) -> double {
+      const double ef = md.idx_efac >= 0 ? pget(q, md.idx_efac) : md.efac_const;
+      const double ef2 = ef * ef;
+      double sl = 0.0, sq = 0.0;
+      for (int t = threadIdx.x; t < n; t += LBLK) {
+        const double N0 = ef2 * md.sig2[t] + Q;
+        sl += log(N0);
+        sq += wc[t] / N0;
+      }
+      sl = block_sum(sl, red);
+      sq = block_sum(sq, red);
+      return -0.5 * ((la + sl) + sq);
+    };
+    double Qx = exp(2.0 * pget(xv, md.idx_equad) * 2.302585092994045684);
+    double l0 = lnl(xv, Qx), p0 = lnprior4(md, xv);
+    if (a.eval_only) {
+      if (threadIdx.x == 0) a.out_w[c] = l0;
+    } else {
+      for (int step = 0; step < NWHITE; ++step) {
+        const int par = (int)mhv[step][0];
+        double q[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[j] = (j == par) ? xv[j] + mhv[step][1] : xv[j];
+        const double Qq = (par == md.idx_equad) ? Qx * mhv[step][3] : Qx;
+        const double p1 = lnprior4(md, q);
+        if (p1 == -INFINITY) continue;
+        const double l1 = lnl(q, Qq);
+        if ((l1 + p1) - (l0 + p0) > mhv[step][2]) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) xv[j] = q[j];
+          l0 = l1;
+          p0 = p1;
+          Qx = Qq;
+        }
+      }
+      if (threadIdx.x < md.P) a.st.x[(size_t)c * md.P + threadIdx.x] = pget(xv, threadIdx.x);
+    }
+  }
+  __syncthreads();
+  // N^-1, sum log N, r^T N^-1 r at the final white parameters (gibbs.py:297,309-312)
+  const double ef = md.idx_efac >= 0 ? pget(xv, md.idx_efac) : md.efac_const;
+  const double ef2 = ef * ef;
+  const double Q = exp(2.0 * pget(xv, md.idx_equad) * 2.302585092994045684);
+  double sl = 0.0, sr = 0.0;
+  for (int t = threadIdx.x; t < npad; t += LBLK) {
+    double wt = 0.0;
+    if (t < n) {
+      const double N = (zc[t] != 0.0 ? alc[t] : 1.0) * (ef2 * md.sig2[t] + Q);
+      sl += log(N);
+      sr += md.resid[t] * md.resid[t] / N;
+      wt = 1.0 / N;
+    }
+    wc[t] = wt;
+  }
+  sl = block_sum(sl, red);
+  sr = block_sum(sr, red);
+  if (threadIdx.x == 0) {
+    sc[SC_LOGDETN] = sl;
+    sc[SC_RNR] = sr;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// gram: G_c = T_aug^T diag(w_c) T_aug, lower 16x16 tiles, fp64 MFMA 16x16x4
+// ------------------------------------------------------------------------------------
+// Workgroup = 8 waves = 8 chains sharing one 64x64 super-tile (I, J) of the Gram: the T
+// operands of every k-step are the same addresses for all 8 waves (L1/L2 hits), each wave
+// scales its A operand by its own chain's weights.  16 accumulators per wave.
+__global__ void __launch_bounds__(64 * GRAM_WAVES) lg_gram(const DevModel* __restrict__ mds,
+                                                           LArgs a, int nsb, int npairs) {
+  const DevModel& md = mds[0];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int pair = blockIdx.x % npairs;
+  const int c = (blockIdx.x / npairs) * GRAM_WAVES + wv;
+  if (c >= a.C) return;
+  int I = 0;
+  while ((I + 1) * (I + 2) / 2 <= pair) ++I;
+  const int J = pair - I * (I + 1) / 2;
+  const int NT = md.mp / 16;
+  const int nks = md.nks;
+  const double* wc = a.s.w + (size_t)c * md.npad;
+  const int tl = lane >> 4;
+
+  v4d acc[4][4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) acc[u][v] = (v4d){0.0, 0.0, 0.0, 0.0};
+  // tiles beyond NT read tile NT-1 (valid memory) and are never stored
+  int xi[4], yj[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    xi[u] = min(4 * I + u, NT - 1);
+    yj[u] = min(4 * J + u, NT - 1);
+  }
+  const double* Tb = md.Tmf + lane;
+  double ta[4], tb[4], na[4], nb[4], wt, nw;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    ta[u] = Tb[xi[u] * 64];
+    tb[u] = Tb[yj[u] * 64];
+  }
+  wt = wc[tl];
+  const bool diag = (I == J);
+#pragma unroll 1
+  for (int ks = 0; ks < nks; ++ks) {
+    if (ks + 1 < nks) {
+      const double* src = Tb + (size_t)(ks + 1) * NT * 64;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        na[u] = src[xi[u] * 64];
+        nb[u] = src[yj[u] * 64];
+      }
+      nw = wc[4 * (ks + 1) + tl];
+    }
+    double aw[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) aw[u] = ta[u] * wt;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        if (!diag || v <= u) acc[u][v] = __builtin_amdgcn_mfma_f64_16x16x4f64(aw[u], tb[v], acc[u][v], 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      ta[u] = na[u];
+      tb[u] = nb[u];
+    }
+    wt = nw;
+  }
+  double* Gc = a.s.G + (size_t)c * md.mp * md.mp;
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int X = 4 * I + u, Y = 4 * J + v;
+      if (X >= NT || Y >= NT || (diag && v > u)) continue;
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        Gc[(size_t)(16 * X + tl + 4 * g) * md.mp + 16 * Y + (lane & 15)] = acc[u][v][g];
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// tmelim: eliminate the timing-model columns [0, K0) of G (LDL^T-scaled, raw columns)
+// ------------------------------------------------------------------------------------
+// Panels of 16 columns: the panel (rows k0..mp) is factored in LDS, written back, then the
+// trailing lower triangle is updated by MFMA: G_ij -= sum_kk P_i,kk P_j,kk / a_kk.
+__global__ void __launch_bounds__(LBLK) lg_tmelim(const DevModel* __restrict__ mds, LArgs a) {
+  const int c = blockIdx.x;
+  const DevModel& md = mds[0];
+  extern __shared__ double lsm[];
+  constexpr int PS = TM_PW + 1;        // panel row stride
+  double* P = lsm;                     // [mp][PS]
+  __shared__ double ainv[TM_PW];
+  __shared__ double red[4];
+  const int mp = md.mp, K0 = md.ntm_pad, raug = md.raug;
+  double* Gc = a.s.G + (size_t)c * mp * mp;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  double ld = 0.0, quad = 0.0;
+  int fail = 0;
+  for (int k0 = 0; k0 < K0; k0 += TM_PW) {
+    const int R = mp - k0;
+    // load the panel; timing-model prior 1/tm_weight on its diagonal, unit pivots on pads
+    for (int e = tid; e < R * TM_PW; e += LBLK) {
+      const int i = e / TM_PW, kk = e % TM_PW;
+      const int gi = k0 + i, gk = k0 + kk;
+      double v = (gi >= gk) ? Gc[(size_t)gi * mp + gk] : 0.0;
+      if (gi == gk) v = (gk < md.ntm) ? v + md.tm_phiinv : 1.0;
+      P[i * PS + kk] = v;
+    }
+    __syncthreads();
+    // factor the panel (columns kk, rows kk..R)
+    for (int kk = 0; kk < TM_PW; ++kk) {
+      const double akk = P[kk * PS + kk];
+      const double r = 1.0 / akk;
+      for (int e = tid; e < (R - kk - 1) * (TM_PW - kk - 1); e += LBLK) {
+        const int i = kk + 1 + e / (TM_PW - kk - 1);
+        const int j = kk + 1 + e % (TM_PW - kk - 1);
+        if (j <= i) P[i * PS + j] -= P[i * PS + kk] * (P[j * PS + kk] * r);
+      }
+      if (tid == 0) {
+        fail |= !(akk > 0.0) ? 1 : 0;
+        ld += log(akk);
+        const double zr = P[(raug - k0) * PS + kk];
+        quad += zr * zr * r;
+        ainv[kk] = r;
+      }
+      __syncthreads();
+    }
+    // write the raw panel back (columns k0..k0+16, rows >= column)
+    for (int e = tid; e < R * TM_PW; e += LBLK) {
+      const int i = e / TM_PW, kk = e % TM_PW;
+      if (i >= kk) Gc[(size_t)(k0 + i) * mp + k0 + kk] = P[i * PS + kk];
+    }
+    // trailing update of rows/cols >= k1 by MFMA tiles (wave-strided over lower tiles)
+    const int k1 = k0 + TM_PW;
+    const int TR = (mp - k1) / 16;
+    const int ntile = TR * (TR + 1) / 2;
+    for (int e = wv; e < ntile; e += LBLK / 64) {
+      int X = 0;
+      while ((X + 1) * (X + 2) / 2 <= e) ++X;
+      const int Y = e - X * (X + 1) / 2;
+      const int r0 = k1 + 16 * X, c0 = k1 + 16 * Y;
+      v4d acc;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[g] = Gc[(size_t)(r0 + (lane >> 4) + 4 * g) * mp + c0 + (lane & 15)];
+#pragma unroll
+      for (int k4 = 0; k4 < TM_PW / 4; ++k4) {
+        const int kk = 4 * k4 + (lane >> 4);
+        const double av = -P[(r0 - k0 + (lane & 15)) * PS + kk];
+        const double bv = P[(c0 - k0 + (lane & 15)) * PS + kk] * ainv[kk];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) Gc[(size_t)(r0 + (lane >> 4) + 4 * g) * mp + c0 + (lane & 15)] = acc[g];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    double* sc = a.s.sc + (size_t)c * 16;
+    sc[SC_LDTM] = ld;
+    sc[SC_QUADTM] = quad;
+    sc[SC_FAILTM] = (double)fail;
+  }
+  (void)red;
+}
+
+// ------------------------------------------------------------------------------------
+// hyper: red-noise MH on S0 + diag(phi^-1) in LDS; b draw's Fourier block
+// ------------------------------------------------------------------------------------
+struct HyperLds {
+  double* S;    // [ms][SS] working factor (raw columns), row-major lower
+  int SS;
+};
+
+__global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ mds, LArgs a) {
+  const int c = blockIdx.x;
+  const DevModel& md = mds[0];
+  extern __shared__ double lsm[];
+  const int nf = md.nf, K0 = md.ntm_pad, mp = md.mp;
+  const int ms = nf + 1;               // Fourier block + augmented row
+  const int SS = ms + 1;
+  double* S = lsm;                     // [ms][SS]
+  double* ph = S + ms * SS;            // [nf] phi^-1
+  double* vv = ph + nf;                // [ms] back-substitution accumulators / Delta
+  double* wv_ = vv + ms;               // [ms] rhs
+  __shared__ double red[4];
+  __shared__ double mhv[NHYPER][4];
+  __shared__ double bc[4];
+  const int tid = threadIdx.x;
+  double* sc = a.s.sc + (size_t)c * 16;
+  const double* Gc = a.s.G + (size_t)c * mp * mp;
+  const Rng rng = make_rng(a, c);
+  const double* tp = tape_row(a, c);
+  double xv[4];
+  load_x(md, a.st, c, xv);
+  const double logdetN = sc[SC_LOGDETN], rNr = sc[SC_RNR];
+  const double ld_tm = sc[SC_LDTM], quad_tm = sc[SC_QUADTM];
+  const int fail_tm = sc[SC_FAILTM] != 0.0;
+  const double x_last0 = sc[SC_XLAST];
+  int status = fail_tm ? 1 : 0;
+  if (!a.eval_only && tid < NHYPER) mh_variate(md, rng, tp, NWHITE + tid, mhv[tid]);
+
+  // factor S0 + diag(phi^-1(q)) in LDS; returns the b-marginalised lnL (gibbs.py:288-329)
+  auto lnl = [&](const double (&q)[4], int& failed) -> double {
+    const double lA = pget(q, md.idx_logA);
+    const double g = pget(q, md.idx_gamma);
+    const double lc = 2.0 * lA * 2.302585092994045684 - md.log_12pi2 + (g - 3.0) * md.log_fyr;
+    for (int f = tid; f < nf; f += LBLK) ph[f] = exp(-(lc - g * md.lfreq[f] + md.ldf[f]));
+    const double logdet_phi = ((double)nf * lc - g * md.sum_lfreq + md.sum_ldf) + md.logdet_phi_tm;
+    __syncthreads();
+    for (int e = tid; e < ms * ms; e += LBLK) {
+      const int i = e / ms, j = e % ms;
+      if (j > i) continue;
+      const int gi = (i < nf) ? K0 + i : md.raug, gj = K0 + j;
+      double v = Gc[(size_t)gi * mp + gj];
+      if (i == j && i < nf) v += ph[i];
+      S[i * SS + j] = v;
+    }
+    __syncthreads();
+    double ld = 0.0, quad = 0.0;
+    int fl = 0;
+    for (int k = 0; k < nf; ++k) {
+      const double akk = S[k * SS + k];
+      const double r = 1.0 / akk;
+      const double zr = S[nf * SS + k];
+      fl |= !(akk > 0.0) ? 1 : 0;
+      ld += log(akk);
+      quad += zr * zr * r;
+      // rows i in (k, nf], cols j in (k, i]: 32 row groups x 8 column groups
+      const int i0 = k + 1 + (tid >> 3), j0 = k + 1 + (tid & 7);
+      for (int i = i0; i < ms; i += 32) {
+        const double lik = S[i * SS + k] * r;
+        for (int j = j0; j <= i; j += 8) S[i * SS + j] -= lik * S[j * SS + k];
+      }
+      __syncthreads();
+    }
+    failed = fl | fail_tm;
+    if (failed) return -INFINITY;
+    double ll = -0.5 * (logdetN + rNr);
+    ll += 0.5 * ((quad_tm + quad) - (ld_tm + ld) - logdet_phi);
+    return ll;
+  };
+
+  const bool run = (a.mask & 6u) || a.eval_only;
+  bool redraw = false, Lvalid = false;
+  int fb = 0;
+  if (run) {
+    __syncthreads();
+    double l0 = 0.0, p0 = 0.0;
+    const int first = ((a.mask & 2u) || a.eval_only) ? -1 : NHYPER;
+    for (int step = first; step <= NHYPER; ++step) {
+      double q[4], luacc = 0.0;
+      if (step == NHYPER) {
+        if (a.eval_only || !(a.mask & 4u)) break;
+        redraw = true;
+        for (int j = 0; j < md.P; ++j) redraw = redraw && (xv[j] != x_last0);   // gibbs.py:373
+        if (a.mask & 128u) redraw = true;
+        if (!redraw || Lvalid) break;
+      }
+      if (step < 0 || step == NHYPER) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[j] = xv[j];
+      } else {
+        const int par = (int)mhv[step][0];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[j] = (j == par) ? xv[j] + mhv[step][1] : xv[j];
+        luacc = mhv[step][2];
+      }
+      const double p1 = lnprior4(md, q);
+      if (step >= 0 && step < NHYPER && p1 == -INFINITY) continue;
+      int f1 = 0;
+      const double l1 = lnl(q, f1);
+      if (step == NHYPER) {
+        fb = f1;
+        break;
+      }
+      if (f1) status |= 1;
+      if (step < 0) {
+        l0 = l1;
+        p0 = p1;
+        Lvalid = true;
+        if (a.eval_only) {
+          if (tid == 0) a.out_h[c] = l1;
+          break;
+        }
+        continue;
+      }
+      if ((l1 + p1) - (l0 + p0) > luacc) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xv[j] = q[j];
+        l0 = l1;
+        p0 = p1;
+        Lvalid = true;
+      } else {
+        Lvalid = false;
+      }
+    }
+  }
+  if (a.eval_only) return;
+  if (tid < md.P) a.st.x[(size_t)c * md.P + tid] = pget(xv, tid);
+  if (tid == 0) {
+    sc[SC_REDRAW] = redraw ? 1.0 : 0.0;
+    sc[SC_FB] = (double)fb;
+    if (a.st.status) a.st.status[c] |= status | ((redraw && fb) ? 2 : 0);
+  }
+  if (!redraw || fb) return;
+  // b draw, Fourier block: w_k = zraw_k y_k + eta_k, then L^T v = w (raw columns, pivots on
+  // the diagonal, y_k = 1/sqrt(a_kk)); back substitution in axpy form over rows of S
+  double* vF = a.s.v + (size_t)c * mp + K0;
+  if (tp) {
+    for (int i = tid; i < nf; i += LBLK) vv[i] = 0.0;
+    __syncthreads();
+    for (int j = tid; j < md.m; j += LBLK) {
+      const int ii = md.ref2int[j] - K0;
+      if (ii >= 0 && ii < nf) vv[ii] = tp[TP_DELTA + j];
+    }
+    __syncthreads();
+    // eta_k = y_k sum_{i >= k} a_ik Delta_i (so that L^-T eta = Delta)
+    for (int k = tid; k < nf; k += LBLK) {
+      double s = 0.0;
+      for (int i = k; i < nf; ++i) s += S[i * SS + k] * vv[i];
+      const double yk = rsqrt_nr(S[k * SS + k]);
+      wv_[k] = (S[nf * SS + k] + s) * yk;
+    }
+  } else {
+    for (int k = tid; k < nf; k += LBLK)
+      wv_[k] = S[nf * SS + k] * rsqrt_nr(S[k * SS + k]) +
+               normal_from(rng, (uint32_t)(K0 + k), TAG_BDRAW);
+  }
+  __syncthreads();
+  for (int k = tid; k < nf; k += LBLK) vv[k] = 0.0;   // acc_k = sum_{i>k} a_ik v_i
+  __syncthreads();
+  for (int i = nf - 1; i >= 0; --i) {
+    if (tid == 0) {
+      const double yi = rsqrt_nr(S[i * SS + i]);
+      bc[0] = (wv_[i] - yi * vv[i]) * yi;
+    }
+    __syncthreads();
+    const double vi = bc[0];
+    if (tid == 0) vF[i] = vi;
+    for (int k = tid; k < i; k += LBLK) vv[k] += S[i * SS + k] * vi;
+    __syncthreads();
+  }
+  (void)red;
+}
+
+// ------------------------------------------------------------------------------------
+// btm: b draw's timing-model block, L^T v = w over columns [0, K0) with rows up to raug
+// ------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(LBLK) lg_btm(const DevModel* __restrict__ mds, LArgs a) {
+  const int c = blockIdx.x;
+  const DevModel& md = mds[0];
+  extern __shared__ double lsm[];
+  const int K0 = md.ntm_pad, mp = md.mp, raug = md.raug;
+  double* acc = lsm;          // [K0]
+  double* wk = acc + K0;      // [K0]
+  double* vt = wk + K0;       // [K0] solution, timing-model block
+  double* dl = vt + K0;       // [raug] Delta (tape mode)
+  __shared__ double bc[2];
+  const int tid = threadIdx.x;
+  const double* sc = a.s.sc + (size_t)c * 16;
+  if (sc[SC_REDRAW] == 0.0 || sc[SC_FB] != 0.0) return;
+  const double* Gc = a.s.G + (size_t)c * mp * mp;
+  double* v = a.s.v + (size_t)c * mp;
+  const Rng rng = make_rng(a, c);
+  const double* tp = tape_row(a, c);
+  // acc_k = sum over Fourier rows i of a_ik v_i  (rows of G contiguous in k)
+  for (int k = tid; k < K0; k += LBLK) {
+    double s = 0.0;
+    for (int i = K0; i < raug; ++i) s += Gc[(size_t)i * mp + k] * v[i];
+    acc[k] = s;
+  }
+  if (tp) {
+    for (int i = tid; i < raug; i += LBLK) dl[i] = 0.0;
+    __syncthreads();
+    for (int j = tid; j < md.m; j += LBLK) dl[md.ref2int[j]] = tp[TP_DELTA + j];
+    __syncthreads();
+    for (int k = tid; k < K0; k += LBLK) {
+      double s = 0.0;
+      for (int i = k; i < raug; ++i) s += Gc[(size_t)i * mp + k] * dl[i];
+      const double yk = rsqrt_nr(Gc[(size_t)k * mp + k]);
+      wk[k] = (Gc[(size_t)raug * mp + k] + s) * yk;
+    }
+  } else {
+    for (int k = tid; k < K0; k += LBLK)
+      wk[k] = Gc[(size_t)raug * mp + k] * rsqrt_nr(Gc[(size_t)k * mp + k]) +
+              normal_from(rng, (uint32_t)k, TAG_BDRAW);
+  }
+  __syncthreads();
+  for (int i = K0 - 1; i >= 0; --i) {
+    if (tid == 0) {
+      const double yi = rsqrt_nr(Gc[(size_t)i * mp + i]);
+      bc[0] = (wk[i] - yi * acc[i]) * yi;
+    }
+    __syncthreads();
+    const double vi = bc[0];
+    if (tid == 0) vt[i] = vi;
+    const double* row = Gc + (size_t)i * mp;
+    for (int k = tid; k < i; k += LBLK) acc[k] += row[k] * vi;
+    __syncthreads();
+  }
+  // b in reference order (Fourier part from lg_hyper in v, timing-model part in vt)
+  for (int j = tid; j < md.m; j += LBLK) {
+    const int ii = md.ref2int[j];
+    a.st.b[(size_t)c * md.m + j] = ii < K0 ? vt[ii] : v[ii];
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// tb: y = r - T b for every chain (gibbs.py:213,237,272) as one MFMA GEMM
+// ------------------------------------------------------------------------------------
+// Wave: 16 chains x 64 TOAs (4 tiles); A = b (chains x basis), B = T^T (basis x TOAs) read
+// from the column-major Tcol so a wave's B fragment is 16 consecutive TOAs.
+__global__ void __launch_bounds__(LBLK) lg_tb(const DevModel* __restrict__ mds, LArgs a) {
+  const DevModel& md = mds[0];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int t0 = blockIdx.x * 64;
+  const int cb = (blockIdx.y * 4 + wv) * 16;
+  if (cb >= a.C) return;
+  const int m = md.m, npad = md.npad;
+  const int ci = cb + (lane & 15);
+  const bool cok = ci < a.C;
+  const double* bc = a.st.b + (size_t)(cok ? ci : cb) * m;
+  v4d acc[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) acc[u] = (v4d){0.0, 0.0, 0.0, 0.0};
+  const int kl = lane >> 4;
+#pragma unroll 2
+  for (int k = 0; k < m; k += 4) {
+    const int j = k + kl;
+    const bool jok = j < m;
+    const double av = (cok && jok) ? bc[j] : 0.0;
+    const double* tc = md.Tcol + (size_t)(jok ? j : 0) * npad + t0 + (lane & 15);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const double bv = jok ? tc[16 * u] : 0.0;
+      acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[u], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int cc = cb + kl + 4 * g;
+      const int t = t0 + 16 * u + (lane & 15);
+      if (cc < a.C && t < npad)
+        a.s.y[(size_t)cc * npad + t] = (t < md.n) ? md.resid[t] - acc[u][g] : 0.0;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// toa: theta, z, alpha, nu (gibbs.py:185-259)
+// ------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(LBLK) lg_toa(const DevModel* __restrict__ mds, LArgs a) {
+  const int c = blockIdx.x;
+  const DevModel& md = mds[0];
+  __shared__ double red[4];
+  __shared__ double dfb[32];
+  const int n = md.n, nst = a.st.nst, m = md.m, tid = threadIdx.x;
+  double* zc = a.st.z + (size_t)c * nst;
+  double* alc = a.st.alpha + (size_t)c * nst;
+  double* poc = a.st.pout + (size_t)c * nst;
+  const double* yc = a.s.y + (size_t)c * md.npad;
+  const Rng rng = make_rng(a, c);
+  const double* tp = tape_row(a, c);
+  double xv[4];
+  load_x(md, a.st, c, xv);
+  double theta = a.st.theta[c], nu = a.st.nu[c];
+  const double ef = md.idx_efac >= 0 ? pget(xv, md.idx_efac) : md.efac_const;
+  const double ef2 = ef * ef;
+  const double Q = exp(2.0 * pget(xv, md.idx_equad) * 2.302585092994045684);
+  const bool mix = (md.model == 2) || (md.model == 3);
+  if ((a.mask & 8u) && mix) {
+    double zs = 0.0;
+    for (int t = tid; t < n; t += LBLK) zs += (zc[t] != 0.0) ? 1.0 : 0.0;
+    zs = block_sum(zs, red);
+    const double aa = zs + md.mk;
+    const double bb = ((double)n - zs) + md.k1mm;
+    if (tp) {
+      theta = tp[TP_DELTA + m];
+    } else {
+      const double ga = gamma_mt(aa, rng, 0u, TAG_THETA);
+      const double gb = gamma_mt(bb, rng, 1u, TAG_THETA);
+      theta = ga / (ga + gb);
+    }
+  }
+  if ((a.mask & 16u) && mix) {
+    const double SQ2PI = 2.5066282746310002;  // np.sqrt(2*np.pi)
+    for (int t = tid; t < n; t += LBLK) {
+      const double N0 = ef2 * md.sig2[t] + Q;
+      const double Nv = alc[t] * N0;
+      const double y = yc[t];
+      const double sd1 = sqrt(Nv);
+      const double x1 = y / sd1;
+      double top = theta * (exp(-(x1 * x1) / 2.0) / SQ2PI / sd1);
+      if (md.model == 3) top = theta / md.pspin;
+      const double sd0 = sqrt(N0);
+      const double x0 = y / sd0;
+      const double bot = top + (1.0 - theta) * (exp(-(x0 * x0) / 2.0) / SQ2PI / sd0);
+      double qz = top / bot;
+      if (isnan(qz)) qz = 1.0;
+      poc[t] = qz;
+      const double pz = qz < 1.0 ? qz : 1.0;
+      double u;
+      if (tp) {
+        u = tp[TP_DELTA + m + 1 + t];
+      } else {
+        double unused;
+        rng.uniform2((uint32_t)t, TAG_Z, u, unused);
+      }
+      zc[t] = (double)bern_legacy(pz, u);
+    }
+  }
+  __syncthreads();
+  if ((a.mask & 32u) && md.vary_alpha) {
+    double zs = 0.0;
+    for (int t = tid; t < n; t += LBLK) zs += (zc[t] != 0.0) ? 1.0 : 0.0;
+    zs = block_sum(zs, red);
+    if (zs >= 1.0) {
+      for (int t = tid; t < n; t += LBLK) {
+        const double zf = zc[t] != 0.0 ? 1.0 : 0.0;
+        const double N0 = ef2 * md.sig2[t] + Q;
+        const double top = ((yc[t] * yc[t]) * zf / N0 + nu) / 2.0;
+        const double G = tp ? tp[TP_DELTA + m + 1 + nst + t]
+                            : gamma_mt((zf + nu) / 2.0, rng, (uint32_t)t, TAG_ALPHA);
+        alc[t] = top / G;
+      }
+    }
+  }
+  __syncthreads();
+  if ((a.mask & 64u) && md.vary_df) {
+    double sa = 0.0;
+    for (int t = tid; t < n; t += LBLK) sa += log(alc[t]) + 1.0 / alc[t];
+    const double S = block_sum(sa, red);
+    if (tid < 64) {
+      double ll = -INFINITY;
+      if (tid < 30) {
+        const double h = (double)(tid + 1) / 2.0;
+        ll = -h * S + md.dfA[tid] - md.dfB[tid];
+      }
+      const double mx = wave_max(ll);
+      if (tid < 30) dfb[tid] = exp(ll - mx);
+    }
+    __syncthreads();
+    double u;
+    if (tp) {
+      u = tp[TP_DELTA + m + 1 + 2 * nst];
+    } else {
+      double unused;
+      rng.uniform2(0u, TAG_DF, u, unused);
+    }
+    double acc8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc8[j] = dfb[j];
+#pragma unroll
+    for (int i = 8; i < 24; i += 8)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc8[j] += dfb[i + j];
+    double tot = ((acc8[0] + acc8[1]) + (acc8[2] + acc8[3])) + ((acc8[4] + acc8[5]) + (acc8[6] + acc8[7]));
+#pragma unroll
+    for (int i = 24; i < 30; ++i) tot += dfb[i];
+    double cdf[30];
+    double cs = 0.0;
+#pragma unroll
+    for (int i = 0; i < 30; ++i) {
+      cs += dfb[i] / tot;
+      cdf[i] = cs;
+    }
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < 30; ++i) cnt += (cdf[i] / cdf[29] <= u) ? 1 : 0;
+    cnt = cnt < 29 ? cnt : 29;
+    nu = (double)(cnt + 1);
+  }
+  if (tid == 0) {
+    a.st.theta[c] = theta;
+    a.st.nu[c] = nu;
+  }
+}
+
+}  // namespace gst

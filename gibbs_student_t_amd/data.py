@@ -152,5 +152,32 @@ def simulate_data(seed: int, theta: float = 0.05, sigma_out: float = 1e-6,
     return out, clean
 
 
-__all__ = ["load_j1713_raw", "design_matrix", "simulate_residuals", "j1713", "simulate_data",
+def scaled_synthetic(n: int = 100_000, components: int = 60, ntm: int = 300, seed: int = 5,
+                     years: float = 10.0, theta: float = 0.05, sigma_out: float = 1e-6,
+                     log10_A: float = -14.0, gamma: float = 4.33) -> PulsarData:
+    """BASELINE config 5 ("scaled synthetic: 100k TOAs, 60 red-noise Fourier modes + 300
+    timing/DMX columns, m ~ 420") -- not in the reference; built with its recipe:
+
+    TOAs uniform over ``years``, log-normal error bars 10^(-7 + 0.2 xi) s
+    (simulate_data.py:15), power-law red noise, Bernoulli(theta) outliers with sigma_out
+    (simulate_data.py:24-26), and a random ``ntm``-column timing/DMX design matrix whose
+    span is projected out of the residuals (its SVD basis is orthonormal, run_sims.py:22-25).
+    """
+    rng = np.random.default_rng(seed)
+    t0 = 53000.0 * DAY_SEC
+    toas = np.sort(t0 + rng.uniform(0.0, years * 365.25 * DAY_SEC, n))
+    err = 10 ** (-7 + rng.standard_normal(n) * 0.2)
+    tt = (toas - toas.mean()) / (toas.max() - toas.min())
+    # a few smooth spin/astrometry-like columns, then random DMX-like columns
+    M = [np.ones(n), tt, tt ** 2]
+    M += [rng.standard_normal(n) for _ in range(max(0, ntm - 3))]
+    M = np.column_stack(M[:ntm])
+    U = np.linalg.svd(M, full_matrices=False)[0]
+    r, z = simulate_residuals(toas, err, U, theta=theta, sigma_out=sigma_out,
+                              log10_A=log10_A, gamma=gamma, components=components, rng=rng)
+    return PulsarData(name="SIM", toas=toas, residuals=r, toaerrs=err, Mmat=M,
+                      meta={"z_true": z, "seed": seed, "theta": theta})
+
+
+__all__ = ["load_j1713_raw", "scaled_synthetic", "design_matrix", "simulate_residuals", "j1713", "simulate_data",
            "FYR"]

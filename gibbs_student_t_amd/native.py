@@ -89,7 +89,7 @@ class NativeSampler:
     record arrays are laid out with row stride ``self.n`` = the largest n of the batch.
     """
 
-    def __init__(self, pta, cfg: dict, device: int = 0):
+    def __init__(self, pta, cfg: dict, device: int = 0, path: str = "auto"):
         torch = _torch()
         self.lib = _abi.load()
         if not torch.cuda.is_available():
@@ -104,6 +104,9 @@ class NativeSampler:
         _abi.check(self.lib, self.lib.gst_ctx_create(self.device, ct.byref(ctx)),
                    "gst_ctx_create")
         self.ctx = ctx
+        if path not in _abi.PATHS:
+            raise ValueError(f"path must be one of {sorted(_abi.PATHS)}")
+        _abi.check(self.lib, self.lib.gst_set_path(self.ctx, _abi.PATHS[path]), "gst_set_path")
         self.ptas, self.cfgs = ptas, [dict(c) for c in cfgs]
         self.pta, self.cfg = ptas[0], self.cfgs[0]
         descs, self._keep = [], []
@@ -118,6 +121,9 @@ class NativeSampler:
         _abi.check(self.lib, self.lib.gst_model_info(self.ctx, ct.byref(nd), ct.byref(nmax),
                                                      ct.byref(stride)), "gst_model_info")
         self.ndatasets = nd.value
+        pth = ct.c_int()
+        _abi.check(self.lib, self.lib.gst_get_path(self.ctx, ct.byref(pth)), "gst_get_path")
+        self.path = {v: k for k, v in _abi.PATHS.items()}[pth.value]
         self.n_of = [int(p_.T.shape[0]) for p_ in ptas]
         self.n, self.m = nmax.value, int(ptas[0].T.shape[1])
         self.P = len(ptas[0].params)
@@ -221,6 +227,18 @@ class NativeSampler:
         _abi.check(self.lib, self.lib.gst_last_sweep_ms(self.ctx, ct.byref(ms)),
                    "gst_last_sweep_ms")
         return ms.value
+
+    def set_timing(self, on: bool = True):
+        """Per-kernel HIP-event timing of the large path (kernel_times())."""
+        _abi.check(self.lib, self.lib.gst_set_timing(self.ctx, int(bool(on))), "gst_set_timing")
+
+    def kernel_times(self):
+        """{kind: (total ms, launches)} for the last launch with timing enabled."""
+        k = len(_abi.KERNEL_KINDS)
+        ms = (ct.c_double * k)()
+        nl = (ct.c_int * k)()
+        _abi.check(self.lib, self.lib.gst_kernel_times(self.ctx, ms, nl, k), "gst_kernel_times")
+        return {name: (ms[i], nl[i]) for i, name in enumerate(_abi.KERNEL_KINDS)}
 
     def close(self):
         if getattr(self, "ctx", None):

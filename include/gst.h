@@ -167,6 +167,26 @@ int gst_eval_lnlike(void* ctx, const gst_state* state, int nchains, double* out_
 
 int gst_sync(void* ctx, void* stream);
 
+/* Execution path.  The persistent path keeps a whole chain in one wavefront for all of a
+ * launch's sweeps (n <= 256, m <= ~78: J1713+0747-sized pulsars); the large path runs
+ * each sweep as a pipeline of kernels (fp64-MFMA Gram shared by all chains, blocked
+ * timing-model elimination, LDS-resident red-noise MH, MFMA T b, per-TOA passes) for
+ * large n and m (BASELINE config 5).  AUTO (default) picks persistent when it fits.
+ * gst_set_path must precede gst_model_set. */
+enum gst_path { GST_PATH_AUTO = 0, GST_PATH_PERSISTENT = 1, GST_PATH_LARGE = 2 };
+int gst_set_path(void* ctx, int path);
+int gst_get_path(void* ctx, int* path);
+
+/* Per-kernel timing of the large path (HIP events around every launch of the next
+ * gst_sweep / gst_eval_lnlike calls while enabled).  gst_kernel_times fills ms[k] (summed
+ * milliseconds) and launches[k] for kernel kinds k < nkinds (enum gst_kernel_kind). */
+enum gst_kernel_kind {
+  GST_K_RECORD = 0, GST_K_WHITE = 1, GST_K_GRAM = 2, GST_K_TMELIM = 3,
+  GST_K_HYPER = 4, GST_K_BTM = 5, GST_K_TB = 6, GST_K_TOA = 7, GST_K_COUNT = 8
+};
+int gst_set_timing(void* ctx, int on);
+int gst_kernel_times(void* ctx, double* ms, int* launches, int nkinds);
+
 /* Diagnostic builds (-DGST_STAMPS) only: per-chain per-stage s_memtime cycle sums are
  * accumulated into dev_buf[C][8]; returns an error in production builds. */
 int gst_debug_stamps(void* ctx, unsigned long long* dev_buf);

@@ -30,7 +30,7 @@ def load_ref(name):
     d = dict(np.load(os.path.join(GOLDEN, f"ref_{name}.npz"), allow_pickle=False))
     d["kw"] = ast.literal_eval(str(d.pop("model_kw")))
     d["tape"] = {k[5:]: v for k, v in d.items() if k.startswith("tape_")}
-    ds = name.split("_")[0] if name.split("_")[0] in ("sim", "twob", "simclean") else "j1713"
+    ds = name.split("_")[0] if name.split("_")[0] in ("sim", "twob", "simclean", "scaled") else "j1713"
     d["pta"] = load_dataset(efac="efac" in name, dataset=ds)
     return d
 

@@ -26,8 +26,14 @@ NAMES = fixture_names()
 RTOL = 1e-10
 
 
-def _native(ref, C):
-    ns = NativeSampler(ref["pta"], ref["kw"], 0)
+PATHS = ("persistent", "large")
+
+
+def _native(ref, C, path="auto"):
+    if path == "persistent" and ref["pta"].T.shape[1] + 1 > 80:
+        pytest.skip("beyond the persistent kernel's shapes (large path only)")
+    ns = NativeSampler(ref["pta"], ref["kw"], 0, path=path)
+    assert path == "auto" or ns.path == path
     ns.alloc(C)
     return ns
 
@@ -45,7 +51,8 @@ def _states(ref, idx):
 
 
 @pytest.mark.parametrize("name", NAMES)
-def test_lnlikelihoods(name):
+@pytest.mark.parametrize("path", PATHS)
+def test_lnlikelihoods(name, path):
     """get_lnlikelihood_white / get_lnlikelihood at every point the reference evaluated."""
     ref = load_ref(name)
     tape = ref["tape"]
@@ -55,7 +62,7 @@ def test_lnlikelihoods(name):
         st, ss = _states(ref, idx)
         xs = tape[f"{which}_lnl_x"].reshape(S * K, -1)
         want = tape[f"{which}_lnl"].reshape(-1)
-        ns = _native(ref, S * K)
+        ns = _native(ref, S * K, path)
         ns.set_state(x=xs, theta=np.array([s["theta"] for s in ss]),
                      nu=np.array([s["nu"] for s in ss]), **st)
         w, h = ns.eval_lnlike()
@@ -79,13 +86,14 @@ def test_lnlikelihoods(name):
 
 
 @pytest.mark.parametrize("name", NAMES)
-def test_mh_blocks_and_b_draw(name):
+@pytest.mark.parametrize("path", PATHS)
+def test_mh_blocks_and_b_draw(name, path):
     """White MH + Gram + hyper MH + b draw, each sweep from the reference's start state."""
     ref = load_ref(name)
     S = int(ref["niter"])
     idx = np.arange(S)
     st, ss = _states(ref, idx)
-    ns = _native(ref, S)
+    ns = _native(ref, S, path)
     ns.set_state(x=ref["chain"][:S], theta=np.array([s["theta"] for s in ss]),
                  nu=np.array([s["nu"] for s in ss]), **st)
     rows = pack_tape(ref["tape"], idx, ns.n, ns.m, ns.stride)
@@ -122,14 +130,15 @@ def test_mh_blocks_and_b_draw(name):
 
 
 @pytest.mark.parametrize("name", NAMES)
-def test_outlier_stages(name):
+@pytest.mark.parametrize("path", PATHS)
+def test_outlier_stages(name, path):
     """theta, z, alpha, nu from the reference's post-b state (gibbs.py:377-380)."""
     ref = load_ref(name)
     S = int(ref["niter"]) - 1
     idx = np.arange(S)
     pre = [sweep_state(ref, i) for i in idx]
     post = [sweep_state(ref, i + 1) for i in idx]
-    ns = _native(ref, S)
+    ns = _native(ref, S, path)
     ns.set_state(x=ref["chain"][1:S + 1], b=np.stack([s["b"] for s in post]),
                  z=np.stack([s["z"] for s in pre]), alpha=np.stack([s["alpha"] for s in pre]),
                  pout=np.stack([s["pout"] for s in pre]),
@@ -150,12 +159,13 @@ def test_outlier_stages(name):
 
 
 @pytest.mark.parametrize("name", [n for n in NAMES if "fixed" in n and "vvh17" not in n])
-def test_full_chain_replay(name):
+@pytest.mark.parametrize("path", PATHS)
+def test_full_chain_replay(name, path):
     """12 consecutive sweeps of one chain on the reference's tape (gibbs.py:342-385)."""
     ref = load_ref(name)
     S = int(ref["niter"])
     s0 = sweep_state(ref, 0)
-    ns = _native(ref, 1)
+    ns = _native(ref, 1, path)
     ns.set_state(x=ref["xs"][None], b=s0["b"][None], z=s0["z"][None],
                  alpha=s0["alpha"][None], pout=s0["pout"][None], theta=np.array([s0["theta"]]),
                  nu=np.array([s0["nu"]]))
@@ -174,10 +184,11 @@ def test_full_chain_replay(name):
         assert np.all(r <= tol), f"{k}: max rel {r.max():.3e}"
 
 
-def test_philox_mode_runs_and_moves():
+@pytest.mark.parametrize("path", PATHS)
+def test_philox_mode_runs_and_moves(path):
     ref = load_ref("beta_fixed")
     C, S = 256, 50
-    ns = _native(ref, C)
+    ns = _native(ref, C, path)
     s0 = sweep_state(ref, 0)
     ns.set_state(x=np.tile(ref["xs"], (C, 1)), b=np.tile(s0["b"], (C, 1)),
                  z=np.tile(s0["z"], (C, 1)), alpha=np.tile(s0["alpha"], (C, 1)),
@@ -197,7 +208,8 @@ def test_philox_mode_runs_and_moves():
     assert np.all((x >= lo) & (x <= hi)), names
 
 
-def test_sharding_invariance():
+@pytest.mark.parametrize("path", PATHS)
+def test_sharding_invariance(path):
     """Chains keyed by global id: one launch of C == two launches of C/2 (bitwise)."""
     ref = load_ref("uniform_prior")
     C, S = 16, 5
@@ -206,15 +218,43 @@ def test_sharding_invariance():
                 z=np.tile(s0["z"], (C, 1)), alpha=np.tile(s0["alpha"], (C, 1)),
                 pout=np.tile(s0["pout"], (C, 1)), theta=np.full(C, s0["theta"]),
                 nu=np.full(C, s0["nu"]))
-    ns = _native(ref, C)
+    ns = _native(ref, C, path)
     ns.set_state(**init)
     ns.sweep(S, seed=99, sweep0=7)
     full = ns.get_state()
     halves = []
     for h in range(2):
-        nh = _native(ref, C // 2)
+        nh = _native(ref, C // 2, path)
         nh.set_state(**{k: v[h * C // 2:(h + 1) * C // 2] for k, v in init.items()})
         nh.sweep(S, seed=99, sweep0=7, chain0=h * C // 2)
         halves.append(nh.get_state())
     for k in ("x", "b", "z", "alpha", "pout", "theta", "nu"):
         np.testing.assert_array_equal(full[k], np.concatenate([h[k] for h in halves]))
+
+
+def test_paths_agree_in_philox_mode():
+    """Both paths draw the same Philox variates: J1713 chains follow the same MH/z/nu
+    decisions (floating-point differences are ~1e-13, far from any decision threshold)."""
+    ref = load_ref("beta_prior")
+    C, S = 64, 6
+    s0 = sweep_state(ref, 0)
+    lo = np.array([p.pmin for p in ref["pta"].params])
+    hi = np.array([p.pmax for p in ref["pta"].params])
+    init = dict(x=np.random.default_rng(3).uniform(lo, hi, size=(C, len(lo))),
+                b=np.tile(s0["b"], (C, 1)), z=np.tile(s0["z"], (C, 1)),
+                alpha=np.tile(s0["alpha"], (C, 1)), pout=np.tile(s0["pout"], (C, 1)),
+                theta=np.full(C, s0["theta"]), nu=np.full(C, s0["nu"]))
+    out = {}
+    for path in PATHS:
+        ns = _native(ref, C, path)
+        ns.set_state(**init)
+        ns.sweep(S, seed=5, sweep0=2)
+        out[path] = ns.get_state()
+        ns.close()
+    a, b = out["persistent"], out["large"]
+    same = np.all(a["x"] == b["x"], axis=1) & np.all(a["z"] == b["z"], axis=1) & \
+        (a["nu"] == b["nu"])
+    assert same.mean() >= 0.95, same.mean()
+    for k in ("b", "alpha", "pout", "theta"):
+        r = _rel(b[k][same], a[k][same])
+        assert np.all(r <= 1e-8), f"{k}: max rel {r.max():.3e}"

@@ -300,11 +300,30 @@ def simclean(niter=12):
               file=sys.stderr)
 
 
+def scaled(niter=6):
+    """A mid-size cut of BASELINE config 5 (gdata.scaled_synthetic): n = 1500 TOAs,
+    40 red-noise components (80 Fourier columns) + 100 timing/DMX columns, m = 180 --
+    beyond the register-resident kernel, exercising the multi-kernel large path."""
+    psr = gdata.scaled_synthetic(n=1500, components=40, ntm=100, seed=11)
+    pta6 = PTA(psr, components=40)
+    np.savez_compressed(os.path.join(OUTDIR, "scaled_dataset.npz"), **dataset_arrays(pta6, psr))
+    for name in ("beta", "t"):
+        out = run_one(pta6, name, MODELS[name], seed=3300 + len(name), niter=niter,
+                      x0=[4.33, -14.0, -7.6])
+        out["model_kw"] = np.array(repr(MODELS[name]))
+        np.savez_compressed(os.path.join(OUTDIR, f"ref_scaled_{name}_fixed.npz"), **out)
+        print("scaled", name, "n", pta6.n, "m", pta6.m, "cond:",
+              np.nanmax(out["tape_b_cond"]), file=sys.stderr)
+
+
 def main():
     os.makedirs(OUTDIR, exist_ok=True)
     niter = 12
     if "--only-simclean" in sys.argv:
         simclean(niter)
+        return
+    if "--only-scaled" in sys.argv:
+        scaled()
         return
     psr = gdata.j1713(seed=1713, theta=0.05)
     pta = PTA(psr)
@@ -347,6 +366,7 @@ def main():
     out["model_kw"] = np.array(repr(MODELS["uniform"]))
     np.savez_compressed(os.path.join(OUTDIR, "ref_twob_uniform_fixed.npz"), **out)
     simclean(niter)
+    scaled()
 
 
 if __name__ == "__main__":
