@@ -153,6 +153,20 @@ def workload(config: int, rank: int, world: int, chains: int | None):
                           "Gaussian and Student-t nu=4 white noise, outlier + no_outlier "
                           "twins, 5 outlier models) x 64 chains, 32 datasets per GPU, fp64"),
                     data="simulate_data.py restatement per dataset (seeded), ragged n")
+    if config == 5:
+        psr = data.scaled_synthetic(n=100_000, components=60, ntm=300, seed=5)
+        pta = PTA(psr, components=60)
+        C = chains or 512
+        c0 = rank * C
+        return dict(ptas=[pta], cfgs=[CFG], ds=np.zeros(C, np.int32),
+                    init=initial_state(pta, C, c0), chain0=c0, C=C, per=C,
+                    desc=("scaled synthetic pulsar: 100k TOAs over 10 yr, 60 red-noise "
+                          "components (120 Fourier columns) + 300 timing/DMX columns (m=420), "
+                          "run_sims 'beta' model, 512 chains per GPU, fp64, large-model path"),
+                    data=("data.scaled_synthetic: log-normal error bars, power-law red noise, "
+                          "5% outliers, random 300-column timing/DMX design matrix projected "
+                          "out; records x, b, theta, nu every sweep (per-TOA chains not "
+                          "recorded: 1.2 GB per sweep)"))
     raise SystemExit(f"unknown --config {config}")
 
 
@@ -161,7 +175,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=300)
-    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4),
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5),
                     help="BASELINE.json config (2 = headline J1713+0747, 1024 chains/GPU)")
     ap.add_argument("--chains", type=int, default=None,
                     help="chains per GPU (config 4: per dataset)")
@@ -196,7 +210,11 @@ def main():
     ns.set_state(**wl["init"])
     if W > 0:
         ns.sweep(W, seed=args.seed, sweep0=0, chain0=c0)
-    rec = ns.alloc_records(K)
+    large = ns.path == "large"
+    rec = ns.alloc_records(K, keys=("x", "b", "theta", "nu") if large else
+                           ("x", "b", "z", "alpha", "pout", "theta", "nu"))
+    if large:
+        ns.set_timing(True)
     torch.cuda.synchronize(dev)
     dist.barrier(dev)
     torch.cuda.synchronize(dev)
@@ -207,6 +225,7 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     kernel_ms = ns.last_kernel_ms()
+    ktimes = ns.kernel_times() if large else None
     status = ns.get_state()["status"]
 
     # ESS per dataset (its chains share one posterior), summed over datasets and ranks
@@ -242,6 +261,15 @@ def main():
         n_eff = n if args.config != 4 else n_mean
         flops = algorithmic_flops(n_eff, m) * C * K
         achieved = flops / (kernel_ms * 1e-3) / 1e12
+        stages = None
+        if ktimes:
+            # dominant kernel = the Gram; its algorithmic flops per launch are the
+            # n (m+1) (m+2) term of the fixed formula x chains (one launch per sweep)
+            g_ms, g_n = ktimes["gram"]
+            gram_flop = n_eff * (m + 1) * (m + 2) * C
+            achieved = gram_flop / (g_ms / g_n * 1e-3) / 1e12
+            stages = {k: {"ms_per_sweep": v[0] / max(1, K), "launches": v[1]}
+                      for k, v in ktimes.items()}
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc) and args.config == 2:
@@ -250,7 +278,8 @@ def main():
                 traffic = pj["hbm_bytes_per_chain_sweep"] * C * K
             except Exception:
                 traffic = None
-        min_ess = float(min(v for v in ess_tot.values() if v > 0))
+        pos = [v for v in ess_tot.values() if v > 0]
+        min_ess = float(min(pos)) if pos else None
         out = {
             "metric": METRIC,
             "value": value,
@@ -270,7 +299,7 @@ def main():
                        "record_every": 1,
                        "parallelism": f"independent chains sharded over {world} GPU(s); "
                                       "RCCL only for the final summary all-reduce"},
-            "ess_per_sec": min_ess / elapsed,
+            "ess_per_sec": (min_ess / elapsed) if min_ess else None,
             "ess_total": {k: float(v) for k, v in ess_tot.items()},
             "rhat_max": {k: float(v) for k, v in rhat_max.items()},
             "chains_with_status": int(s_vec[-1]),
@@ -278,11 +307,15 @@ def main():
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
                          "traffic": traffic,
+                         "kernel": "lg_gram (per-launch HIP events)" if large else
+                                   "gst_sweep_kernel (persistent, whole launch)",
                          "algorithmic_flop_per_chain_sweep": algorithmic_flops(n_eff, m),
                          "toa_pass_GBps": toa_pass_bytes(n_eff) * C * K / (kernel_ms * 1e-3)
                          / 1e9},
             "cpu_baseline": cpu,
         }
+        if stages:
+            out["stages"] = stages
         print(json.dumps(out), flush=True)
     ns.close()
     dist.finalize()

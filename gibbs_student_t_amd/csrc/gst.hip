@@ -159,7 +159,8 @@ static int pack_dataset(Ctx* cx, const gst_model_desc* d, gst::DevModel& md, int
   for (int j = 0; j < m; ++j) int2ref[ref2int[j]] = j;
   const int NT = mpad / 16;
   const int nks = round_up(n, 4) / 4;
-  std::vector<double> Tmf((size_t)nks * NT * 64, 0.0);
+  // k-steps padded with zeros to whole 64-TOA chunks (the large path's Gram stages 16)
+  std::vector<double> Tmf((size_t)(npad / 4) * NT * 64, 0.0);
   for (int ks = 0; ks < nks; ++ks)
     for (int X = 0; X < NT; ++X)
       for (int l = 0; l < 64; ++l) {
@@ -402,6 +403,8 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
     const int ms = h.nf + 1;
     cx->lds_hyper = (size_t)(ms * (ms + 1) + h.nf + 2 * ms) * 8;
     cx->lds_btm = (size_t)(3 * h.ntm_pad + h.raug) * 8;
+    HIP_OK(hipFuncSetAttribute((const void*)gst::lg_gram,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, gst::GRAM_LDS * 8));
     HIP_OK(hipFuncSetAttribute((const void*)gst::lg_tmelim,
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)cx->lds_tm));
     HIP_OK(hipFuncSetAttribute((const void*)gst::lg_hyper,
@@ -495,7 +498,8 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
     LG_LAUNCH(GST_K_WHITE, gst::lg_white, g_chain, b_chain, 0);
     if ((mask & 6u) || eval_only) {
       if (ev_mark(cx, GST_K_GRAM, st, true)) return -1;
-      hipLaunchKernelGGL(gst::lg_gram, g_gram, b_gram, 0, st, cx->dmd, a, nsb, npairs);
+      hipLaunchKernelGGL(gst::lg_gram, g_gram, b_gram, gst::GRAM_LDS * 8, st, cx->dmd, a, nsb,
+                         npairs);
       HIP_OK(hipGetLastError());
       if (ev_mark(cx, GST_K_GRAM, st, false)) return -1;
       LG_LAUNCH(GST_K_TMELIM, gst::lg_tmelim, g_chain, b_chain, cx->lds_tm);

@@ -265,72 +265,107 @@ __global__ void __launch_bounds__(LBLK) lg_white(const DevModel* __restrict__ md
 // ------------------------------------------------------------------------------------
 // gram: G_c = T_aug^T diag(w_c) T_aug, lower 16x16 tiles, fp64 MFMA 16x16x4
 // ------------------------------------------------------------------------------------
-// Workgroup = 8 waves = 8 chains sharing one 64x64 super-tile (I, J) of the Gram: the T
-// operands of every k-step are the same addresses for all 8 waves (L1/L2 hits), each wave
-// scales its A operand by its own chain's weights.  16 accumulators per wave.
+// Workgroup = 8 waves = 8 chains sharing one 64x64 super-tile (I, J) of the Gram.  The T
+// operands (8 column tiles x 16 k-steps = 64 TOAs = 64 KB) are staged cooperatively in LDS,
+// double-buffered: chunk i+1 is fetched into registers while chunk i feeds the MFMAs, so
+// every T element is read from L2/HBM once per workgroup and the MFMAs never wait on a
+// global load.  Each wave scales its A operand by its own chain's weights (LDS too).
+constexpr int GRAM_KC = 16;                       // k-steps (of 4 TOAs) per chunk
+constexpr int GRAM_LDS = 2 * GRAM_KC * 8 * 64 + 2 * GRAM_WAVES * 64;   // doubles
+
 __global__ void __launch_bounds__(64 * GRAM_WAVES) lg_gram(const DevModel* __restrict__ mds,
                                                            LArgs a, int nsb, int npairs) {
   const DevModel& md = mds[0];
-  const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int pair = blockIdx.x % npairs;
-  const int c = (blockIdx.x / npairs) * GRAM_WAVES + wv;
-  if (c >= a.C) return;
-  int I = 0;
-  while ((I + 1) * (I + 2) / 2 <= pair) ++I;
-  const int J = pair - I * (I + 1) / 2;
+  extern __shared__ double lsm[];
+  double* Tl = lsm;                               // [2][KC][8 tiles][64]
+  double* Wl = lsm + 2 * GRAM_KC * 8 * 64;        // [2][8 waves][64]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // block order: pair-major (the chain groups of one super-tile run together and share its
+  // T columns in L2), off-diagonal super-tiles first, the shorter diagonal ones last
+  const int ngroups = (a.C + GRAM_WAVES - 1) / GRAM_WAVES;
+  const int prank = blockIdx.x / ngroups;
+  const int cg = (blockIdx.x % ngroups) * GRAM_WAVES + wv;
+  const bool live = cg < a.C;
+  const int c = live ? cg : a.C - 1;              // dead waves still stage and sync
+  const int noff = npairs - nsb;
+  int I, J;
+  if (prank < noff) {                              // (I, J), I > J, row-major
+    I = 1;
+    while (I * (I + 1) / 2 <= prank) ++I;
+    J = prank - I * (I - 1) / 2;
+  } else {
+    I = J = prank - noff;
+  }
   const int NT = md.mp / 16;
-  const int nks = md.nks;
+  const int nu = min(4, NT - 4 * I), nv = min(4, NT - 4 * J);   // valid tiles of the block
+  const int nch = md.npad / (4 * GRAM_KC);
   const double* wc = a.s.w + (size_t)c * md.npad;
   const int tl = lane >> 4;
+  const bool diag = (I == J);
+
+  // staging map: 512 threads x 8 double2 = 8 tiles x 16 k-steps x 32 double2
+  int gcol[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) gcol[u] = min(u < 4 ? 4 * I + u : 4 * J + u - 4, NT - 1);
+  typedef double v2d __attribute__((ext_vector_type(2)));
+  v2d stg[8];
+  double wstg;
+  auto fetch = [&](int ch) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int e = tid + 512 * r;
+      const int q = e & 31, u = (e >> 5) & 7, k = e >> 8;
+      const size_t ks = (size_t)ch * GRAM_KC + k;
+      stg[r] = *(const v2d*)(md.Tmf + (ks * NT + gcol[u]) * 64 + 2 * q);
+    }
+    wstg = wc[(size_t)ch * 64 + lane];
+  };
+  auto stash = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int e = tid + 512 * r;
+      const int q = e & 31, u = (e >> 5) & 7, k = e >> 8;
+      *(v2d*)(Tl + ((buf * GRAM_KC + k) * 8 + u) * 64 + 2 * q) = stg[r];
+    }
+    Wl[(buf * GRAM_WAVES + wv) * 64 + lane] = wstg;
+  };
 
   v4d acc[4][4];
 #pragma unroll
   for (int u = 0; u < 4; ++u)
 #pragma unroll
     for (int v = 0; v < 4; ++v) acc[u][v] = (v4d){0.0, 0.0, 0.0, 0.0};
-  // tiles beyond NT read tile NT-1 (valid memory) and are never stored
-  int xi[4], yj[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    xi[u] = min(4 * I + u, NT - 1);
-    yj[u] = min(4 * J + u, NT - 1);
-  }
-  const double* Tb = md.Tmf + lane;
-  double ta[4], tb[4], na[4], nb[4], wt, nw;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    ta[u] = Tb[xi[u] * 64];
-    tb[u] = Tb[yj[u] * 64];
-  }
-  wt = wc[tl];
-  const bool diag = (I == J);
+  fetch(0);
+  stash(0);
+  __syncthreads();
 #pragma unroll 1
-  for (int ks = 0; ks < nks; ++ks) {
-    if (ks + 1 < nks) {
-      const double* src = Tb + (size_t)(ks + 1) * NT * 64;
+  for (int ch = 0; ch < nch; ++ch) {
+    const int buf = ch & 1;
+    if (ch + 1 < nch) fetch(ch + 1);
+    const double* Tb = Tl + buf * GRAM_KC * 8 * 64 + lane;
+    const double* Wb = Wl + (buf * GRAM_WAVES + wv) * 64 + tl;
+#pragma unroll 4
+    for (int k = 0; k < GRAM_KC; ++k) {
+      const double wt = Wb[4 * k];
+      double aw[4], tb[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        na[u] = src[xi[u] * 64];
-        nb[u] = src[yj[u] * 64];
+        aw[u] = Tb[(k * 8 + u) * 64] * wt;
+        tb[u] = Tb[(k * 8 + 4 + u) * 64];
       }
-      nw = wc[4 * (ks + 1) + tl];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          if ((!diag || v <= u) && u < nu && v < nv)
+            acc[u][v] = __builtin_amdgcn_mfma_f64_16x16x4f64(aw[u], tb[v], acc[u][v], 0, 0, 0);
     }
-    double aw[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) aw[u] = ta[u] * wt;
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int v = 0; v < 4; ++v)
-        if (!diag || v <= u) acc[u][v] = __builtin_amdgcn_mfma_f64_16x16x4f64(aw[u], tb[v], acc[u][v], 0, 0, 0);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      ta[u] = na[u];
-      tb[u] = nb[u];
-    }
-    wt = nw;
+    if (ch + 1 < nch) stash(buf ^ 1);
+    __syncthreads();
   }
+  if (!live) return;
   double* Gc = a.s.G + (size_t)c * md.mp * md.mp;
 #pragma unroll
   for (int u = 0; u < 4; ++u)
