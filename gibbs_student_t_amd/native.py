@@ -161,7 +161,7 @@ class NativeSampler:
             if v is None:
                 continue
             t = self.state[k]
-            src = torch.as_tensor(np.asarray(v, dtype=np.float64)).reshape(t.shape)
+            src = torch.from_numpy(np.array(v, dtype=np.float64)).reshape(t.shape)
             t.copy_(src.to(self.tdev))
 
     def get_state(self):

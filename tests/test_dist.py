@@ -50,3 +50,58 @@ def test_single_process_is_identity():
     s, m = dist.reduce_summary(np.array([1.0, 2.0]), np.array([3.0]))
     assert s.tolist() == [1.0, 2.0] and m.tolist() == [3.0]
     assert dist.chain_range(3, 1024) == (3072, 4096)
+
+
+def _workload_worker(rank, world, port, out):
+    import sys
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch
+    import torch.distributed as tdist
+
+    import bench
+    r, _, w = dist.init("gloo")
+    res = {}
+    for cfg in (2, 3, 4):
+        wl = bench.workload(cfg, r, w, None)
+        ids = torch.arange(wl["chain0"], wl["chain0"] + wl["C"])
+        allids = [torch.zeros_like(ids) for _ in range(w)]
+        tdist.all_gather(allids, ids)
+        # dataset content per chain: residual checksum of each chain's dataset
+        ck = torch.tensor([float(wl["ptas"][d].get_residuals()[0].sum()) for d in wl["ds"]],
+                          dtype=torch.float64)
+        ent = torch.tensor([wl["chain0"] // wl["per"] + int(d) for d in wl["ds"]])
+        allent = [torch.zeros_like(ent) for _ in range(w)]
+        tdist.all_gather(allent, ent)
+        allck = [torch.zeros_like(ck) for _ in range(w)]
+        tdist.all_gather(allck, ck)
+        res[cfg] = (torch.cat(allids).tolist(), torch.cat(allck).tolist(), wl["C"],
+                    torch.cat(allent).tolist())
+    out.put((r, res))
+    dist.finalize()
+
+
+def test_two_rank_bench_workloads_partition_chains():
+    """bench.py under torch.distributed.run: ranks own disjoint global chain ids (Philox
+    keys) and agree on the data; config 4 shards the run_sims grid by dataset."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_workload_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for cfg in (2, 3, 4):
+        ids, ck, C, _ = res[0][cfg]
+        assert ids == res[1][cfg][0] and ck == res[1][cfg][1]   # both ranks see the same
+        assert ids == list(range(2 * C))                        # disjoint, contiguous
+    # configs 2/3: one dataset replicated on every rank; config 4: different datasets
+    ck2 = res[0][2][1]
+    assert len(set(ck2)) == 1
+    ent4, C4 = res[0][4][3], res[0][4][2]
+    assert set(ent4[:C4]).isdisjoint(set(ent4[C4:]))          # run_sims entries sharded
+    assert sorted(set(ent4)) == list(range(64))               # 32 per rank, 64 chains each
