@@ -789,7 +789,93 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
     GST_STAMP(0)
 
     // ---- white-noise MH block (gibbs.py:114-143); step -1 = the initial lnlike0
-    if ((mask & 1u) || eval_only) {
+    if ((mask & 1u) && !eval_only && md.ncls > 0) {
+      // Noise-class path: a likelihood is a few scalar ops (no TOA reduction), so the
+      // block is a serial chain of log/divide latencies.  Evaluate it speculatively:
+      // for the next D steps, lane 2^j - 1 + b evaluates step s0+j's proposal on the
+      // accept/reject path b (bit i = step s0+i accepted); the decisions are then read
+      // back lane by lane.  Every value is computed with the sequential code's exact
+      // operation order, so the decisions and the final state are bitwise identical.
+      white_prep();
+      constexpr int D = 6;
+      double Wu[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) Wu[u] = (u < md.ncls) ? rdlane(wcls, u) : 0.0;
+      auto lnl_lane = [&](const double (&xq)[4], double Q) __attribute__((always_inline)) -> double {
+        const double ef2 = efac2_of(xq);
+        if (md.ncls == 1) {
+          const double N0 = ef2 * md.csig2[0] + Q;
+          return -0.5 * ((wcls_la + md.ccount[0] * log(N0)) + Wu[0] / N0);
+        }
+        double sl = 0.0, sq = 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (u < md.ncls) {
+            const double N0 = ef2 * md.csig2[u] + Q;
+            sl += md.ccount[u] * log(N0);
+            sq += Wu[u] / N0;
+          }
+        }
+        return -0.5 * ((sl + wcls_la) + sq);
+      };
+      double Qx = exp(2.0 * pget(xv, md.idx_equad) * 2.302585092994045684);
+      double l0 = lnl_lane(xv, Qx), p0 = lnprior(xv);
+#pragma unroll 1
+      for (int s0 = 0; s0 < NWHITE; s0 += D) {
+        const int nd = (NWHITE - s0) < D ? (NWHITE - s0) : D;
+        // this lane's node: level j, path b
+        const int node = lane + 1;
+        const int j = 31 - __builtin_clz(node);          // node in [2^j, 2^(j+1))
+        const int b = node - (1 << j);
+        double xq[4], Q = Qx;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) xq[t] = xv[t];
+        double p1 = -INFINITY, l1 = 0.0;
+        if (j < nd) {
+          for (int i = 0; i < j; ++i) {
+            if ((b >> i) & 1) {
+              const int gs = s0 + i;
+              const int par = (int)mhv[4 * gs + 0];
+              const double delta = mhv[4 * gs + 1];
+#pragma unroll
+              for (int t = 0; t < 4; ++t) xq[t] = (t == par) ? xq[t] + delta : xq[t];
+              if (par == md.idx_equad) Q = Q * mhv[4 * gs + 3];
+            }
+          }
+          double qv[4], E;
+          int par;
+          (void)propose(xq, qv, s0 + j, E, par);
+          const double Qq = (par == md.idx_equad) ? Q * E : Q;
+          p1 = lnprior(qv);
+          if (p1 != -INFINITY) l1 = lnl_lane(qv, Qq);
+        }
+        GST_SUB_BEGIN
+        int path = 0;
+        for (int jj = 0; jj < nd; ++jj) {
+          const int L = (1 << jj) - 1 + path;
+          const double pl = rdlane(p1, L);
+          const double ll = rdlane(l1, L);
+          const double luacc = mhv[4 * (s0 + jj) + 2];
+          if (pl != -INFINITY && (ll + pl) - (l0 + p0) > luacc) {
+            l0 = ll;
+            p0 = pl;
+            path |= 1 << jj;
+          }
+        }
+        GST_SUB_END(15)
+        // apply the accepted moves in order (the sequential code's xv = qv, Qx = Qq)
+        for (int i = 0; i < nd; ++i) {
+          if ((path >> i) & 1) {
+            const int gs = s0 + i;
+            const int par = (int)mhv[4 * gs + 0];
+            const double delta = mhv[4 * gs + 1];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) xv[t] = (t == par) ? xv[t] + delta : xv[t];
+            if (par == md.idx_equad) Qx = Qx * mhv[4 * gs + 3];
+          }
+        }
+      }
+    } else if ((mask & 1u) || eval_only) {
       white_prep();
       double l0 = 0.0, p0 = 0.0;
       double Qx = exp(2.0 * pget(xv, md.idx_equad) * 2.302585092994045684);
