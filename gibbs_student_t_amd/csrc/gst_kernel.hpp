@@ -250,9 +250,10 @@ __device__ double gamma_mt(double a, const Rng& rng, uint32_t index, uint32_t ta
 // buffer of q = k % 8.  Rows <= k are masked on the reading side (only slot K can hold
 // them).  The slot column holding column k+1 is updated first so its publication (the
 // step-to-step dependency through LDS) is issued before the rest of the trailing update.
-// Outputs per column: the pivot a_kk (apiv), the augmented-row entry a_{raug,k} (zraw),
-// sum log a_kk (= log|Sigma| over these columns, as mantissa product + exponent sum) and
-// sum zraw^2 / a_kk (= the d^T Sigma^-1 d contribution).
+// Outputs per column: the pivot a_kk and the augmented-row entry a_{raug,k}, kept by lane
+// k % 64 in cc.apr / cc.zr; chol_stats then gives sum log a_kk (= log|Sigma| over these
+// columns, as mantissa product + exponent sum), sum a_{raug,k}^2 / a_kk (= the
+// d^T Sigma^-1 d contribution) and the failure flag.
 struct CholCtx {
   double* colq;   // [8][MP]
   int lane, p, q, raug;
@@ -328,13 +329,9 @@ __device__ __forceinline__ void chol_step(double (&L)[SL(MT, 0)], CholCtx& cc,
       nxt.sk = rcp_nr1(nxt.akk);
     }
   }
-  // off the critical path: bookkeeping and the rest of the trailing update
-  cc.fail |= !(cur.akk > 0.0) ? 1 : 0;
-  int e;
-  const double mm = frexp(cur.akk, &e);
-  cc.mant *= mm;
-  cc.expo += e;
-  cc.quad = fma(cur.zk * cur.zk, cur.sk, cc.quad);
+  // off the critical path: capture pivot / aug entry (lane k % 64) and the rest of the
+  // trailing update; log|Sigma|, the quad form and the failure flag are reduced from these
+  // lane-parallel after the elimination (chol_stats), not accumulated per step
   cc.apr[k / 64] = (cc.lane == (k & 63)) ? cur.akk : cc.apr[k / 64];
   cc.zr[k / 64] = (cc.lane == (k & 63)) ? cur.zk : cc.zr[k / 64];
   double lrs[MT];
@@ -362,6 +359,36 @@ __device__ __forceinline__ void chol_range(double (&L)[SL(MT, 0)], CholCtx& cc) 
   c.sk = rcp_nr1(c.akk);
   chol_step<MT, KLO, 0, KEND>(L, cc, c);
   lds_order();
+}
+
+// Lane-parallel statistics of an elimination over columns [KLO, KEND) from the per-lane
+// pivots / aug entries (lane k % 64 of apr[k / 64], zr[k / 64]): prod a_kk as mantissa
+// product + exponent sum (log taken once by the caller), sum a_{raug,k}^2 / a_kk and the
+// failure flag, all wave-uniform.  Branch-free on purpose: a lane-divergent region here,
+// inside the register-critical hyper block, makes the allocator spill ~1.4 KB per lane.
+template <int KLO, int KEND>
+__device__ __forceinline__ void chol_stats(CholCtx& cc) {
+  double mm = 1.0, qd = 0.0;
+  int ee = 0, f = 0;
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) {
+    const int j = 64 * sl + cc.lane;
+    const bool in = (j >= KLO) && (j < KEND);
+    const double a = in ? cc.apr[sl] : 1.0, z = in ? cc.zr[sl] : 0.0;
+    f |= !(a > 0.0) ? 1 : 0;
+    int e;
+    mm *= frexp(a, &e);
+    ee += e;
+    qd = fma(z * z, rcp_nr1(a), qd);
+  }
+  mm *= dpp<DPP_XOR1>(mm);
+  mm *= dpp<DPP_XOR2>(mm);
+  mm *= dpp<DPP_ROR4>(mm);
+  mm *= dpp<DPP_ROR8>(mm);
+  cc.mant = (rdlane(mm, 0) * rdlane(mm, 16)) * (rdlane(mm, 32) * rdlane(mm, 48));
+  cc.expo = (int)wave_sum((double)ee);
+  cc.quad = wave_sum(qd);
+  cc.fail = __ballot(f) != 0ull ? 1 : 0;
 }
 
 template <int MT, int NS, int K0, int RA, bool TAPE>
@@ -697,6 +724,7 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
     CholCtx cc{colq, lane, p, q, raug, 1.0, 0.0, 0, 0, {1.0, 1.0}, {0.0, 0.0}};
     GST_SUB_END(10)
     chol_range<MT, 0, 8 * K0>(L, cc);
+    chol_stats<0, 8 * K0>(cc);
     GST_SUB_END(11)
     tm_apr = cc.apr[0];
     tm_zr = cc.zr[0];
@@ -734,6 +762,7 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
     CholCtx cc{colq, lane, p, q, raug, 1.0, 0.0, 0, 0, {tm_apr, 1.0}, {tm_zr, 0.0}};
     GST_SUB_END(7)
     chol_range<MT, K0, RA>(L, cc);
+    chol_stats<8 * K0, RA>(cc);
     GST_SUB_END(8)
     f_apr[0] = cc.apr[0];
     f_apr[1] = cc.apr[1];
