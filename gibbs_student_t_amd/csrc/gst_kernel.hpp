@@ -313,14 +313,15 @@ __device__ __forceinline__ void chol_step(double (&L)[SL(MT, 0)], CholCtx& cc,
   cur.lr[K] = (8 * K + cc.p > k) ? cur.lr[K] : 0.0;
   cur.lc[K] = (8 * K + cc.q > k) ? cur.lc[K] : 0.0;
   ColView<MT> nxt;
+  // lrs = a_ik / a_kk, shared by the critical column and the rest of the trailing update
+  // (the step is fp64-issue-bound: one multiply per row, then one FMA per element)
+  double lrs[MT];
+#pragma unroll
+  for (int r = K; r < MT; ++r) lrs[r] = cur.lr[r] * cur.sk;
   if constexpr (K1 < MT) {
-    // critical path: slot column K1 (holds column k+1).  The products lr*lc need only the
-    // LDS data, the FMA with 1/a_kk only the reciprocal: the two latencies overlap.
-    double t[MT];
+    // critical path: slot column K1 (holds column k+1)
 #pragma unroll
-    for (int r = K1; r < MT; ++r) t[r] = cur.lr[r] * cur.lc[K1];
-#pragma unroll
-    for (int r = K1; r < MT; ++r) L[SL(r, K1)] = fma(-t[r], cur.sk, L[SL(r, K1)]);
+    for (int r = K1; r < MT; ++r) L[SL(r, K1)] = fma(-lrs[r], cur.lc[K1], L[SL(r, K1)]);
     if constexpr (NEXT) {
       chol_publish<MT>(L, cc, K1);
       nxt.akk = rdlane(L[SL(K1, K1)], 9 * KK1);
@@ -334,9 +335,6 @@ __device__ __forceinline__ void chol_step(double (&L)[SL(MT, 0)], CholCtx& cc,
   // lane-parallel after the elimination (chol_stats), not accumulated per step
   cc.apr[k / 64] = (cc.lane == (k & 63)) ? cur.akk : cc.apr[k / 64];
   cc.zr[k / 64] = (cc.lane == (k & 63)) ? cur.zk : cc.zr[k / 64];
-  double lrs[MT];
-#pragma unroll
-  for (int r = K; r < MT; ++r) lrs[r] = cur.lr[r] * cur.sk;
 #pragma unroll
   for (int s = K; s < MT; ++s) {
     if (s == K1 || (KK == 7 && s == K)) continue;  // slot column K is done when KK == 7
