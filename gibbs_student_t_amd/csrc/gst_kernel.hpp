@@ -93,10 +93,14 @@ constexpr int TP_WHITE = 0, TP_HYPER = 80, TP_DELTA = 120;
 
 __host__ __device__ constexpr int SL(int r, int s) { return r * (r + 1) / 2 + s; }
 
-// Stride (doubles) of the per-q column buffers: 8*MT + 2, so that the 16-lane groups of a
-// publishing ds_write_b64 (banks (a/4) mod 32) hit 32 distinct banks (8*MT alone puts the
-// even-q and odd-q lanes 4-way on the same banks).
-__host__ __device__ constexpr int CQ(int MT) { return 8 * MT + 2; }
+// Published-column buffers: colq[q][p][r] (row 8r+p of the column with residue q), r
+// fastest, so a lane's row-side (p) and column-side (q) reads are contiguous in r and go as
+// 128-bit LDS loads.  The publishing stores stay 64-bit: with ds_write_b128 here the
+// same-wave loads that follow returned stale data on MI355X (wrong factors, run-to-run
+// different; measured, round 1), with ds_write_b64 they are exact.  Per-q stride CQ = 8*MT rounded up to 4 mod 32 doubles: with the
+// row stride MT = 10, the 16 lanes (p in {0,1}, q in 0..7) of a publishing ds_write_b128
+// then cover 16 distinct 16-byte bank groups.
+__host__ __device__ constexpr int CQ(int MT) { return 8 * MT + ((4 - 8 * MT) % 32 + 32) % 32; }
 
 #ifdef GST_STAMPS
 #define GST_STAMP_DECL \
@@ -266,10 +270,15 @@ struct CholCtx {
 
 template <int MT>
 __device__ __forceinline__ void chol_publish(const double (&L)[SL(MT, 0)], CholCtx& cc, int s) {
-  double* dst = cc.colq + CQ(MT) * cc.q + cc.p;
+  double* dst = cc.colq + CQ(MT) * cc.q + MT * cc.p;
 #pragma unroll
-  for (int r = 0; r < MT; ++r)
-    if (r >= s) dst[8 * r] = L[SL(r, s)];
+  for (int r2 = 0; r2 < MT; r2 += 2) {          // rows (r2, r2+1)
+    if (r2 >= s) {
+      dst[r2] = L[SL(r2, s)];
+      dst[r2 + 1] = L[SL(r2 + 1, s)];
+    } else if (r2 + 1 >= s)
+      dst[r2 + 1] = L[SL(r2 + 1, s)];
+  }
 }
 
 // 1/a: hardware estimate (~2^-24) + one Newton step (~2e-15 relative, measured on
@@ -290,14 +299,24 @@ struct ColView {
 template <int MT, int K, int KK>
 __device__ __forceinline__ void chol_load(const CholCtx& cc, ColView<MT>& c) {
   const double* col = cc.colq + CQ(MT) * KK;
-  const double* cr = col + cc.p;
-  const double* cq = col + cc.q;
+  const double* cr = col + MT * cc.p;
+  const double* cq = col + MT * cc.q;
 #pragma unroll
-  for (int r = K; r < MT; ++r) {
-    c.lr[r] = cr[8 * r];
-    c.lc[r] = cq[8 * r];
+  for (int r2 = 0; r2 < MT; r2 += 2) {          // rows (r2, r2+1)
+    if (r2 >= K) {  // 128-bit loads (16-byte aligned: CQ, MT, r2 even)
+      typedef double v2_t __attribute__((ext_vector_type(2)));
+      const v2_t a = *(const v2_t*)(cr + r2);
+      const v2_t b = *(const v2_t*)(cq + r2);
+      c.lr[r2] = a[0];
+      c.lr[r2 + 1] = a[1];
+      c.lc[r2] = b[0];
+      c.lc[r2 + 1] = b[1];
+    } else if (r2 + 1 >= K) {
+      c.lr[r2 + 1] = cr[r2 + 1];
+      c.lc[r2 + 1] = cq[r2 + 1];
+    }
   }
-  c.zk = col[cc.raug];
+  c.zk = col[MT * (cc.raug % 8) + cc.raug / 8];
 }
 
 // Step k = 8K + KK, software-pipelined: the slot column holding column k+1 is updated
