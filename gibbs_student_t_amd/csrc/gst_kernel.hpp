@@ -298,6 +298,7 @@ struct ColView {
 
 template <int MT, int K, int KK>
 __device__ __forceinline__ void chol_load(const CholCtx& cc, ColView<MT>& c) {
+  static_assert(MT % 2 == 0 && CQ(MT) % 2 == 0, "128-bit column loads need 16-byte alignment");
   const double* col = cc.colq + CQ(MT) * KK;
   const double* cr = col + MT * cc.p;
   const double* cq = col + MT * cc.q;
