@@ -346,23 +346,46 @@ __global__ void __launch_bounds__(64 * GRAM_WAVES) lg_gram(const DevModel* __res
     if (ch + 1 < nch) fetch(ch + 1);
     const double* Tb = Tl + buf * GRAM_KC * 8 * 64 + lane;
     const double* Wb = Wl + (buf * GRAM_WAVES + wv) * 64 + tl;
-#pragma unroll 4
-    for (int k = 0; k < GRAM_KC; ++k) {
-      const double wt = Wb[4 * k];
-      double aw[4], tb[4];
+    // operands of k-step k+1 are read from LDS before k's MFMAs are issued, so the
+    // lgkmcnt wait is covered by 16 MFMAs (1024 cycles) instead of stalling the wave
+    double ta[4], tb[4], wt = Wb[0];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        aw[u] = Tb[(k * 8 + u) * 64] * wt;
-        tb[u] = Tb[(k * 8 + 4 + u) * 64];
+    for (int u = 0; u < 4; ++u) {
+      ta[u] = Tb[u * 64];
+      tb[u] = Tb[(4 + u) * 64];
+    }
+#pragma unroll
+    for (int k = 0; k < GRAM_KC; ++k) {
+      double na[4], nb[4], nw = 0.0;
+      if (k + 1 < GRAM_KC) {
+        nw = Wb[4 * (k + 1)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          na[u] = Tb[((k + 1) * 8 + u) * 64];
+          nb[u] = Tb[((k + 1) * 8 + 4 + u) * 64];
+        }
       }
+      double aw[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) aw[u] = ta[u] * wt;
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
         for (int v = 0; v < 4; ++v)
           if ((!diag || v <= u) && u < nu && v < nv)
             acc[u][v] = __builtin_amdgcn_mfma_f64_16x16x4f64(aw[u], tb[v], acc[u][v], 0, 0, 0);
+      if (k + 1 < GRAM_KC) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          ta[u] = na[u];
+          tb[u] = nb[u];
+        }
+        wt = nw;
+      }
+      // the other buffer is free since the last barrier: stash the prefetched chunk mid-way
+      // so the wait for its global loads overlaps the second half of this chunk's MFMAs
+      if (k == GRAM_KC / 2 - 1 && ch + 1 < nch) stash(buf ^ 1);
     }
-    if (ch + 1 < nch) stash(buf ^ 1);
     __syncthreads();
   }
   if (!live) return;
