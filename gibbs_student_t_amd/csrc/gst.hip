@@ -484,7 +484,7 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
                eval_only, ow, oh};
   const int nsb = (h.mp / 16 + 3) / 4;
   const int npairs = nsb * (nsb + 1) / 2;
-  const dim3 g_chain(C), b_chain(gst::LBLK);
+  const dim3 g_chain(C), b_chain(gst::LBLK), b_toa(gst::TBLK);
   const dim3 g_gram(npairs * ((C + gst::GRAM_WAVES - 1) / gst::GRAM_WAVES)), b_gram(64 * gst::GRAM_WAVES);
   const dim3 g_tb(h.npad / 64, (C + 63) / 64);
   cx->evused = 0;
@@ -495,7 +495,7 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
   for (int it = 0; it < nit; ++it) {
     a.it = it;
     if (rec_on && it % record_every == 0) LG_LAUNCH(GST_K_RECORD, gst::lg_record, g_chain, b_chain, 0);
-    LG_LAUNCH(GST_K_WHITE, gst::lg_white, g_chain, b_chain, 0);
+    LG_LAUNCH(GST_K_WHITE, gst::lg_white, g_chain, b_toa, 0);
     if ((mask & 6u) || eval_only) {
       if (ev_mark(cx, GST_K_GRAM, st, true)) return -1;
       hipLaunchKernelGGL(gst::lg_gram, g_gram, b_gram, gst::GRAM_LDS * 8, st, cx->dmd, a, nsb,
@@ -510,7 +510,7 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
         LG_LAUNCH(GST_K_TB, gst::lg_tb, g_tb, b_chain, 0);
       }
     }
-    if (!eval_only && (mask & 0x78u)) LG_LAUNCH(GST_K_TOA, gst::lg_toa, g_chain, b_chain, 0);
+    if (!eval_only && (mask & 0x78u)) LG_LAUNCH(GST_K_TOA, gst::lg_toa, g_chain, b_toa, 0);
   }
   HIP_OK(hipEventRecord(cx->ev1, st));
   cx->timed = true;

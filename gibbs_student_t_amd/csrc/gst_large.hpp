@@ -31,6 +31,7 @@
 namespace gst {
 
 constexpr int LBLK = 256;      // threads of the per-chain kernels (4 waves)
+constexpr int TBLK = 1024;     // per-chain per-TOA passes (white, toa): 16 waves hide latency
 constexpr int GRAM_WAVES = 8;  // chains per gram workgroup
 constexpr int TM_PW = 16;      // panel width of the timing-model elimination
 
@@ -78,14 +79,18 @@ __device__ __forceinline__ const double* tape_row(const LArgs& a, int c) {
   return a.tape.data ? a.tape.data + ((size_t)c * a.nsweeps + a.it) * a.tape.stride : nullptr;
 }
 
-// Deterministic block sum (4 waves): every thread gets the bitwise-identical value.
+// Deterministic block sum (NW waves): every thread gets the bitwise-identical value.
+template <int NW = 4>
 __device__ __forceinline__ double block_sum(double v, double* red) {
   v = wave_sum(v);
   const int wv = threadIdx.x >> 6;
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red[wv] = v;
   __syncthreads();
-  return (red[0] + red[1]) + (red[2] + red[3]);
+  double s = 0.0;
+#pragma unroll
+  for (int h = 0; h < NW; h += 4) s += (red[h] + red[h + 1]) + (red[h + 2] + red[h + 3]);
+  return s;
 }
 
 // MH variates of global step gs (0..19 white, 20..29 hyper) exactly as the persistent
@@ -170,10 +175,10 @@ __global__ void __launch_bounds__(LBLK) lg_record(const DevModel* __restrict__ m
 // ------------------------------------------------------------------------------------
 // white: MH over the white-noise parameters, then N^-1 for the Gram
 // ------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(LBLK) lg_white(const DevModel* __restrict__ mds, LArgs a) {
+__global__ void __launch_bounds__(TBLK) lg_white(const DevModel* __restrict__ mds, LArgs a) {
   const int c = blockIdx.x;
   const DevModel& md = mds[0];
-  __shared__ double red[4];
+  __shared__ double red[TBLK / 64];
   __shared__ double mhv[NWHITE][4];
   const int n = md.n, nst = a.st.nst, npad = md.npad;
   const double* zc = a.st.z + (size_t)c * nst;
@@ -191,26 +196,26 @@ __global__ void __launch_bounds__(LBLK) lg_white(const DevModel* __restrict__ md
   if (do_white) {
     // fixed over the block: a_t = alpha_t^z_t, y_t^2 / a_t and sum log a_t
     double la = 0.0;
-    for (int t = threadIdx.x; t < n; t += LBLK) {
+    for (int t = threadIdx.x; t < n; t += TBLK) {
       const bool zt = zc[t] != 0.0;
       const double at = zt ? alc[t] : 1.0;
       if (zt) la += log(at);
       wc[t] = yc[t] * yc[t] / at;
     }
-    la = block_sum(la, red);
+    la = block_sum<TBLK / 64>(la, red);
     if (!a.eval_only && threadIdx.x < NWHITE) mh_variate(md, rng, tp, threadIdx.x, mhv[threadIdx.x]);
     __syncthreads();
     auto lnl = [&](const double (&q)[4], double Q) -> double {
       const double ef = md.idx_efac >= 0 ? pget(q, md.idx_efac) : md.efac_const;
       const double ef2 = ef * ef;
       double sl = 0.0, sq = 0.0;
-      for (int t = threadIdx.x; t < n; t += LBLK) {
+      for (int t = threadIdx.x; t < n; t += TBLK) {
         const double N0 = ef2 * md.sig2[t] + Q;
         sl += log(N0);
         sq += wc[t] / N0;
       }
-      sl = block_sum(sl, red);
-      sq = block_sum(sq, red);
+      sl = block_sum<TBLK / 64>(sl, red);
+      sq = block_sum<TBLK / 64>(sq, red);
       return -0.5 * ((la + sl) + sq);
     };
     double Qx = exp(2.0 * pget(xv, md.idx_equad) * 2.302585092994045684);
@@ -244,7 +249,7 @@ __global__ void __launch_bounds__(LBLK) lg_white(const DevModel* __restrict__ md
   const double ef2 = ef * ef;
   const double Q = exp(2.0 * pget(xv, md.idx_equad) * 2.302585092994045684);
   double sl = 0.0, sr = 0.0;
-  for (int t = threadIdx.x; t < npad; t += LBLK) {
+  for (int t = threadIdx.x; t < npad; t += TBLK) {
     double wt = 0.0;
     if (t < n) {
       const double N = (zc[t] != 0.0 ? alc[t] : 1.0) * (ef2 * md.sig2[t] + Q);
@@ -254,8 +259,8 @@ __global__ void __launch_bounds__(LBLK) lg_white(const DevModel* __restrict__ md
     }
     wc[t] = wt;
   }
-  sl = block_sum(sl, red);
-  sr = block_sum(sr, red);
+  sl = block_sum<TBLK / 64>(sl, red);
+  sr = block_sum<TBLK / 64>(sr, red);
   if (threadIdx.x == 0) {
     sc[SC_LOGDETN] = sl;
     sc[SC_RNR] = sr;
@@ -774,10 +779,10 @@ __global__ void __launch_bounds__(LBLK) lg_tb(const DevModel* __restrict__ mds, 
 // ------------------------------------------------------------------------------------
 // toa: theta, z, alpha, nu (gibbs.py:185-259)
 // ------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(LBLK) lg_toa(const DevModel* __restrict__ mds, LArgs a) {
+__global__ void __launch_bounds__(TBLK) lg_toa(const DevModel* __restrict__ mds, LArgs a) {
   const int c = blockIdx.x;
   const DevModel& md = mds[0];
-  __shared__ double red[4];
+  __shared__ double red[TBLK / 64];
   __shared__ double dfb[32];
   const int n = md.n, nst = a.st.nst, m = md.m, tid = threadIdx.x;
   double* zc = a.st.z + (size_t)c * nst;
@@ -795,8 +800,8 @@ __global__ void __launch_bounds__(LBLK) lg_toa(const DevModel* __restrict__ mds,
   const bool mix = (md.model == 2) || (md.model == 3);
   if ((a.mask & 8u) && mix) {
     double zs = 0.0;
-    for (int t = tid; t < n; t += LBLK) zs += (zc[t] != 0.0) ? 1.0 : 0.0;
-    zs = block_sum(zs, red);
+    for (int t = tid; t < n; t += TBLK) zs += (zc[t] != 0.0) ? 1.0 : 0.0;
+    zs = block_sum<TBLK / 64>(zs, red);
     const double aa = zs + md.mk;
     const double bb = ((double)n - zs) + md.k1mm;
     if (tp) {
@@ -809,7 +814,7 @@ __global__ void __launch_bounds__(LBLK) lg_toa(const DevModel* __restrict__ mds,
   }
   if ((a.mask & 16u) && mix) {
     const double SQ2PI = 2.5066282746310002;  // np.sqrt(2*np.pi)
-    for (int t = tid; t < n; t += LBLK) {
+    for (int t = tid; t < n; t += TBLK) {
       const double N0 = ef2 * md.sig2[t] + Q;
       const double Nv = alc[t] * N0;
       const double y = yc[t];
@@ -837,10 +842,10 @@ __global__ void __launch_bounds__(LBLK) lg_toa(const DevModel* __restrict__ mds,
   __syncthreads();
   if ((a.mask & 32u) && md.vary_alpha) {
     double zs = 0.0;
-    for (int t = tid; t < n; t += LBLK) zs += (zc[t] != 0.0) ? 1.0 : 0.0;
-    zs = block_sum(zs, red);
+    for (int t = tid; t < n; t += TBLK) zs += (zc[t] != 0.0) ? 1.0 : 0.0;
+    zs = block_sum<TBLK / 64>(zs, red);
     if (zs >= 1.0) {
-      for (int t = tid; t < n; t += LBLK) {
+      for (int t = tid; t < n; t += TBLK) {
         const double zf = zc[t] != 0.0 ? 1.0 : 0.0;
         const double N0 = ef2 * md.sig2[t] + Q;
         const double top = ((yc[t] * yc[t]) * zf / N0 + nu) / 2.0;
@@ -853,8 +858,8 @@ __global__ void __launch_bounds__(LBLK) lg_toa(const DevModel* __restrict__ mds,
   __syncthreads();
   if ((a.mask & 64u) && md.vary_df) {
     double sa = 0.0;
-    for (int t = tid; t < n; t += LBLK) sa += log(alc[t]) + 1.0 / alc[t];
-    const double S = block_sum(sa, red);
+    for (int t = tid; t < n; t += TBLK) sa += log(alc[t]) + 1.0 / alc[t];
+    const double S = block_sum<TBLK / 64>(sa, red);
     if (tid < 64) {
       double ll = -INFINITY;
       if (tid < 30) {
