@@ -262,6 +262,7 @@ def main():
         flops = algorithmic_flops(n_eff, m) * C * K
         achieved = flops / (kernel_ms * 1e-3) / 1e12
         stages = None
+        toa_ms = kernel_ms
         if ktimes:
             # dominant kernel = the Gram; its algorithmic flops per launch are the
             # n (m+1) (m+2) term of the fixed formula x chains (one launch per sweep)
@@ -270,12 +271,21 @@ def main():
             achieved = gram_flop / (g_ms / g_n * 1e-3) / 1e12
             stages = {k: {"ms_per_sweep": v[0] / max(1, K), "launches": v[1]}
                       for k, v in ktimes.items()}
+            # per-TOA pass (white MH rescans + theta/z/alpha/nu) over its own kernels' time
+            toa_ms = ktimes["white"][0] + ktimes["toa"][0]
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc) and args.config == 2:
             try:
                 pj = json.load(open(pmc))
                 traffic = pj["hbm_bytes_per_chain_sweep"] * C * K
+            except Exception:
+                traffic = None
+        pmc5 = os.path.join(ROOT, "profiles", "pmc_config5.json")
+        if large and args.config == 5 and os.path.exists(pmc5):
+            try:   # HBM bytes per Gram launch (PMC passes of tools/run_large.py, same shape)
+                g = json.load(open(pmc5))["kernels"]["lg_gram"]
+                traffic = g["hbm_read_bytes"] + g["hbm_write_bytes"]
             except Exception:
                 traffic = None
         pos = [v for v in ess_tot.values() if v > 0]
@@ -310,8 +320,9 @@ def main():
                          "kernel": "lg_gram (per-launch HIP events)" if large else
                                    "gst_sweep_kernel (persistent, whole launch)",
                          "algorithmic_flop_per_chain_sweep": algorithmic_flops(n_eff, m),
-                         "toa_pass_GBps": toa_pass_bytes(n_eff) * C * K / (kernel_ms * 1e-3)
-                         / 1e9},
+                         "toa_pass_GBps": toa_pass_bytes(n_eff) * C * K / (toa_ms * 1e-3) / 1e9,
+                         "toa_pass_hbm_frac": toa_pass_bytes(n_eff) * C * K / (toa_ms * 1e-3)
+                         / 1e9 / HBM_PEAK_GBS},
             "cpu_baseline": cpu,
         }
         if stages:
