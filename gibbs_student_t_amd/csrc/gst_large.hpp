@@ -79,6 +79,36 @@ __device__ __forceinline__ const double* tape_row(const LArgs& a, int c) {
   return a.tape.data ? a.tape.data + ((size_t)c * a.nsweeps + a.it) * a.tape.stride : nullptr;
 }
 
+// Per-thread sum of logs as a running product: mantissa product + exponent sum (v_frexp),
+// one log per thread at the end instead of one per TOA (the per-TOA log dominated the white
+// block's 21 likelihood rescans).  The mantissa product is renormalised every 128 factors
+// (each factor >= 1/2, so it stays far above the fp64 underflow threshold).
+struct LogProd {
+  double mp = 1.0;
+  int ex = 0, k = 0;
+  __device__ __forceinline__ void mul(double v) {
+    int e;
+    mp *= frexp(v, &e);
+    ex += e;
+    if ((++k & 127) == 0) {
+      mp = frexp(mp, &e);
+      ex += e;
+    }
+  }
+  __device__ __forceinline__ double log_sum() const {
+    return log(mp) + (double)ex * 0.693147180559945309417;
+  }
+};
+
+// a / b for positive normal operands without the IEEE division sequence (v_div_scale /
+// v_div_fmas / v_div_fixup): reciprocal estimate, one Newton step, then one residual
+// correction of the quotient (within 1 ulp of the rounded quotient).
+__device__ __forceinline__ double div_pos(double a, double b) {
+  const double y = rcp_nr1(b);
+  const double q0 = a * y;
+  return fma(fma(-b, q0, a), y, q0);
+}
+
 // Deterministic block sum (NW waves): every thread gets the bitwise-identical value.
 template <int NW = 4>
 __device__ __forceinline__ double block_sum(double v, double* red) {
@@ -208,13 +238,14 @@ __global__ void __launch_bounds__(TBLK) lg_white(const DevModel* __restrict__ md
     auto lnl = [&](const double (&q)[4], double Q) -> double {
       const double ef = md.idx_efac >= 0 ? pget(q, md.idx_efac) : md.efac_const;
       const double ef2 = ef * ef;
-      double sl = 0.0, sq = 0.0;
+      double sq = 0.0;
+      LogProd lp;
       for (int t = threadIdx.x; t < n; t += TBLK) {
         const double N0 = ef2 * md.sig2[t] + Q;
-        sl += log(N0);
-        sq += wc[t] / N0;
+        lp.mul(N0);
+        sq += div_pos(wc[t], N0);
       }
-      sl = block_sum<TBLK / 64>(sl, red);
+      const double sl = block_sum<TBLK / 64>(lp.log_sum(), red);
       sq = block_sum<TBLK / 64>(sq, red);
       return -0.5 * ((la + sl) + sq);
     };
@@ -248,18 +279,19 @@ __global__ void __launch_bounds__(TBLK) lg_white(const DevModel* __restrict__ md
   const double ef = md.idx_efac >= 0 ? pget(xv, md.idx_efac) : md.efac_const;
   const double ef2 = ef * ef;
   const double Q = exp(2.0 * pget(xv, md.idx_equad) * 2.302585092994045684);
-  double sl = 0.0, sr = 0.0;
+  double sr = 0.0;
+  LogProd lp;
   for (int t = threadIdx.x; t < npad; t += TBLK) {
     double wt = 0.0;
     if (t < n) {
       const double N = (zc[t] != 0.0 ? alc[t] : 1.0) * (ef2 * md.sig2[t] + Q);
-      sl += log(N);
+      lp.mul(N);
       sr += md.resid[t] * md.resid[t] / N;
       wt = 1.0 / N;
     }
     wc[t] = wt;
   }
-  sl = block_sum<TBLK / 64>(sl, red);
+  const double sl = block_sum<TBLK / 64>(lp.log_sum(), red);
   sr = block_sum<TBLK / 64>(sr, red);
   if (threadIdx.x == 0) {
     sc[SC_LOGDETN] = sl;
@@ -858,8 +890,12 @@ __global__ void __launch_bounds__(TBLK) lg_toa(const DevModel* __restrict__ mds,
   __syncthreads();
   if ((a.mask & 64u) && md.vary_df) {
     double sa = 0.0;
-    for (int t = tid; t < n; t += TBLK) sa += log(alc[t]) + 1.0 / alc[t];
-    const double S = block_sum<TBLK / 64>(sa, red);
+    LogProd lp;
+    for (int t = tid; t < n; t += TBLK) {
+      lp.mul(alc[t]);
+      sa += 1.0 / alc[t];
+    }
+    const double S = block_sum<TBLK / 64>(lp.log_sum() + sa, red);
     if (tid < 64) {
       double ll = -INFINITY;
       if (tid < 30) {
