@@ -310,37 +310,20 @@ __global__ void __launch_bounds__(TBLK) lg_white(const DevModel* __restrict__ md
 constexpr int GRAM_KC = 16;                       // k-steps (of 4 TOAs) per chunk
 constexpr int GRAM_LDS = 2 * GRAM_KC * 8 * 64 + 2 * GRAM_WAVES * 64;   // doubles
 
-__global__ void __launch_bounds__(64 * GRAM_WAVES) lg_gram(const DevModel* __restrict__ mds,
-                                                           LArgs a, int nsb, int npairs) {
-  const DevModel& md = mds[0];
-  extern __shared__ double lsm[];
-  double* Tl = lsm;                               // [2][KC][8 tiles][64]
-  double* Wl = lsm + 2 * GRAM_KC * 8 * 64;        // [2][8 waves][64]
+// Inner loop + store of one super-tile; the valid tile pattern (NU rows of tiles, diagonal
+// or not) is a template parameter, so the 16 MFMAs of a k-step are straight-line code (with
+// the pattern as runtime conditions every MFMA sat behind its own scalar branch).
+template <int NU, bool DIAG>
+__device__ __forceinline__ void gram_tile(const DevModel& md, const LArgs& a, double* Tl,
+                                          double* Wl, int I, int J, int c, bool live) {
+  constexpr int NV = DIAG ? NU : 4;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // block order: pair-major (the chain groups of one super-tile run together and share its
-  // T columns in L2), off-diagonal super-tiles first, the shorter diagonal ones last
-  const int ngroups = (a.C + GRAM_WAVES - 1) / GRAM_WAVES;
-  const int prank = blockIdx.x / ngroups;
-  const int cg = (blockIdx.x % ngroups) * GRAM_WAVES + wv;
-  const bool live = cg < a.C;
-  const int c = live ? cg : a.C - 1;              // dead waves still stage and sync
-  const int noff = npairs - nsb;
-  int I, J;
-  if (prank < noff) {                              // (I, J), I > J, row-major
-    I = 1;
-    while (I * (I + 1) / 2 <= prank) ++I;
-    J = prank - I * (I - 1) / 2;
-  } else {
-    I = J = prank - noff;
-  }
   const int NT = md.mp / 16;
-  const int nu = min(4, NT - 4 * I), nv = min(4, NT - 4 * J);   // valid tiles of the block
   const int nch = md.npad / (4 * GRAM_KC);
   const double* wc = a.s.w + (size_t)c * md.npad;
   const int tl = lane >> 4;
-  const bool diag = (I == J);
 
   // staging map: 512 threads x 8 double2 = 8 tiles x 16 k-steps x 32 double2
   int gcol[8];
@@ -384,12 +367,12 @@ __global__ void __launch_bounds__(64 * GRAM_WAVES) lg_gram(const DevModel* __res
     const double* Tb = Tl + buf * GRAM_KC * 8 * 64 + lane;
     const double* Wb = Wl + (buf * GRAM_WAVES + wv) * 64 + tl;
     // operands of k-step k+1 are read from LDS before k's MFMAs are issued, so the
-    // lgkmcnt wait is covered by 16 MFMAs (1024 cycles) instead of stalling the wave
+    // lgkmcnt wait is covered by the k-step's MFMAs instead of stalling the wave
     double ta[4], tb[4], wt = Wb[0];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      ta[u] = Tb[u * 64];
-      tb[u] = Tb[(4 + u) * 64];
+      ta[u] = u < NU ? Tb[u * 64] : 0.0;
+      tb[u] = u < NV ? Tb[(4 + u) * 64] : 0.0;
     }
 #pragma unroll
     for (int k = 0; k < GRAM_KC; ++k) {
@@ -398,18 +381,18 @@ __global__ void __launch_bounds__(64 * GRAM_WAVES) lg_gram(const DevModel* __res
         nw = Wb[4 * (k + 1)];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          na[u] = Tb[((k + 1) * 8 + u) * 64];
-          nb[u] = Tb[((k + 1) * 8 + 4 + u) * 64];
+          na[u] = u < NU ? Tb[((k + 1) * 8 + u) * 64] : 0.0;
+          nb[u] = u < NV ? Tb[((k + 1) * 8 + 4 + u) * 64] : 0.0;
         }
       }
       double aw[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) aw[u] = ta[u] * wt;
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < NU; ++u)
 #pragma unroll
-        for (int v = 0; v < 4; ++v)
-          if ((!diag || v <= u) && u < nu && v < nv)
+        for (int v = 0; v < NV; ++v)
+          if (!DIAG || v <= u)
             acc[u][v] = __builtin_amdgcn_mfma_f64_16x16x4f64(aw[u], tb[v], acc[u][v], 0, 0, 0);
       if (k + 1 < GRAM_KC) {
 #pragma unroll
@@ -428,15 +411,58 @@ __global__ void __launch_bounds__(64 * GRAM_WAVES) lg_gram(const DevModel* __res
   if (!live) return;
   double* Gc = a.s.G + (size_t)c * md.mp * md.mp;
 #pragma unroll
-  for (int u = 0; u < 4; ++u)
+  for (int u = 0; u < NU; ++u)
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
+    for (int v = 0; v < NV; ++v) {
+      if (DIAG && v > u) continue;
       const int X = 4 * I + u, Y = 4 * J + v;
-      if (X >= NT || Y >= NT || (diag && v > u)) continue;
 #pragma unroll
       for (int g = 0; g < 4; ++g)
         Gc[(size_t)(16 * X + tl + 4 * g) * md.mp + 16 * Y + (lane & 15)] = acc[u][v][g];
     }
+}
+
+__global__ void __launch_bounds__(64 * GRAM_WAVES) lg_gram(const DevModel* __restrict__ mds,
+                                                           LArgs a, int nsb, int npairs) {
+  const DevModel& md = mds[0];
+  extern __shared__ double lsm[];
+  double* Tl = lsm;                               // [2][KC][8 tiles][64]
+  double* Wl = lsm + 2 * GRAM_KC * 8 * 64;        // [2][8 waves][64]
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // block order: pair-major (the chain groups of one super-tile run together and share its
+  // T columns in L2), off-diagonal super-tiles first, the shorter diagonal ones last
+  const int ngroups = (a.C + GRAM_WAVES - 1) / GRAM_WAVES;
+  const int prank = blockIdx.x / ngroups;
+  const int cg = (blockIdx.x % ngroups) * GRAM_WAVES + wv;
+  const bool live = cg < a.C;
+  const int c = live ? cg : a.C - 1;              // dead waves still stage and sync
+  const int noff = npairs - nsb;
+  int I, J;
+  if (prank < noff) {                              // (I, J), I > J, row-major
+    I = 1;
+    while (I * (I + 1) / 2 <= prank) ++I;
+    J = prank - I * (I - 1) / 2;
+  } else {
+    I = J = prank - noff;
+  }
+  const int NT = md.mp / 16;
+  const int nu = min(4, NT - 4 * I);              // valid tile rows (columns: 4 off-diagonal)
+  // wave-uniform dispatch on the tile pattern
+  if (I != J) {
+    switch (nu) {
+      case 4: gram_tile<4, false>(md, a, Tl, Wl, I, J, c, live); break;
+      case 3: gram_tile<3, false>(md, a, Tl, Wl, I, J, c, live); break;
+      case 2: gram_tile<2, false>(md, a, Tl, Wl, I, J, c, live); break;
+      default: gram_tile<1, false>(md, a, Tl, Wl, I, J, c, live); break;
+    }
+  } else {
+    switch (nu) {
+      case 4: gram_tile<4, true>(md, a, Tl, Wl, I, J, c, live); break;
+      case 3: gram_tile<3, true>(md, a, Tl, Wl, I, J, c, live); break;
+      case 2: gram_tile<2, true>(md, a, Tl, Wl, I, J, c, live); break;
+      default: gram_tile<1, true>(md, a, Tl, Wl, I, J, c, live); break;
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------
