@@ -34,6 +34,9 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 // waves (chains) per workgroup: as many as the per-wave LDS footprint allows (one
 // workgroup per CU at these sizes; never more than 4 = one wave per SIMD)
 __host__ __device__ constexpr int wpb_for(int MT, int NS) {
+#ifdef GST_WPB_OVERRIDE  // diagnostic builds only (per-CU contention experiments)
+  return GST_WPB_OVERRIDE;
+#endif
   return (8 * (8 * MT + 2) + 16 * 17 + 64 * NS + 7 * 8 * MT + 32 + 128 +
           64 * ((MT - 2) * (MT - 1) / 2)) * 8 * 4 <= 160 * 1024
              ? 4
@@ -254,17 +257,19 @@ __device__ double gamma_mt(double a, const Rng& rng, uint32_t index, uint32_t ta
 // buffer of q = k % 8.  Rows <= k are masked on the reading side (only slot K can hold
 // them).  The slot column holding column k+1 is updated first so its publication (the
 // step-to-step dependency through LDS) is issued before the rest of the trailing update.
-// Outputs per column: the pivot a_kk and the augmented-row entry a_{raug,k}, kept by lane
-// k % 64 in cc.apr / cc.zr; chol_stats then gives sum log a_kk (= log|Sigma| over these
-// columns, as mantissa product + exponent sum), sum a_{raug,k}^2 / a_kk (= the
+// Outputs per column: the pivot a_kk and the augmented-row entry a_{raug,k}.  Nothing is
+// captured per step (the step is VALU-issue-bound): an eliminated column is frozen in the
+// registers (the column-side mask zeroes every later update to it), so chol_harvest reads
+// both from L after the elimination; chol_stats then gives sum log a_kk (= log|Sigma| over
+// these columns, as mantissa product + exponent sum), sum a_{raug,k}^2 / a_kk (= the
 // d^T Sigma^-1 d contribution) and the failure flag.
 struct CholCtx {
   double* colq;   // [8][MP]
   int lane, p, q, raug;
   double mant, quad;
   int expo, fail;
-  // pivots a_kk and augmented-row entries a_{raug,k}, column k kept by lane k % 64 in
-  // slot k / 64 (registers: no LDS store on the step-to-step critical path)
+  // pivots a_kk and augmented-row entries a_{raug,k}: column k kept by lane k % 64 in
+  // slot k / 64 (filled by chol_harvest)
   double apr[2], zr[2];
 };
 
@@ -293,8 +298,17 @@ __device__ __forceinline__ double rcp_nr1(double a) {
 template <int MT>
 struct ColView {
   double lr[MT], lc[MT];
-  double zk, akk, sk;
+  double akk;
+  double y0, e;  // rcp estimate of 1/a_kk and its Newton residual 1 - a_kk y0
 };
+
+// 1/a_kk in two halves: the estimate and residual start the step's two dependent chains
+// (the critical factor below and the trailing-update reciprocal y0 + y0 e).
+template <int MT>
+__device__ __forceinline__ void pivot_rcp(ColView<MT>& c) {
+  c.y0 = __builtin_amdgcn_rcp(c.akk);
+  c.e = fma(-c.akk, c.y0, 1.0);
+}
 
 template <int MT, int K, int KK>
 __device__ __forceinline__ void chol_load(const CholCtx& cc, ColView<MT>& c) {
@@ -317,7 +331,6 @@ __device__ __forceinline__ void chol_load(const CholCtx& cc, ColView<MT>& c) {
       c.lc[r2 + 1] = cq[r2 + 1];
     }
   }
-  c.zk = col[MT * (cc.raug % 8) + cc.raug / 8];
 }
 
 // Step k = 8K + KK, software-pipelined: the slot column holding column k+1 is updated
@@ -333,28 +346,41 @@ __device__ __forceinline__ void chol_step(double (&L)[SL(MT, 0)], CholCtx& cc,
   cur.lr[K] = (8 * K + cc.p > k) ? cur.lr[K] : 0.0;
   cur.lc[K] = (8 * K + cc.q > k) ? cur.lc[K] : 0.0;
   ColView<MT> nxt;
-  // lrs = a_ik / a_kk, shared by the critical column and the rest of the trailing update
-  // (the step is fp64-issue-bound: one multiply per row, then one FMA per element)
-  double lrs[MT];
-#pragma unroll
-  for (int r = K; r < MT; ++r) lrs[r] = cur.lr[r] * cur.sk;
   if constexpr (K1 < MT) {
-    // critical path: slot column K1 (holds column k+1)
+    // critical path: slot column K1 (holds column k+1).  Its factor a_{8K1+q,k} / a_kk is
+    // one value per lane (lc y0 refined by the Newton term), so the published column
+    // feeds this FMA directly: LDS load -> FMA and rcp -> mul -> FMA -> FMA are the two
+    // step-to-step chains (the row-scaled lrs below stay off them).
+#ifdef GST_EXP_NOLDS  // timing experiment only: critical column without the LDS operands
+    const double t0 = L[SL(K1, K)] * cur.y0;
+    const double tk = fma(t0, cur.e, t0);
 #pragma unroll
-    for (int r = K1; r < MT; ++r) L[SL(r, K1)] = fma(-lrs[r], cur.lc[K1], L[SL(r, K1)]);
+    for (int r = K1; r < MT; ++r) L[SL(r, K1)] = fma(-L[SL(r, K)], tk, L[SL(r, K1)]);
+#else
+    const double t0 = cur.lc[K1] * cur.y0;
+    const double tk = fma(t0, cur.e, t0);
+#pragma unroll
+    for (int r = K1; r < MT; ++r) L[SL(r, K1)] = fma(-cur.lr[r], tk, L[SL(r, K1)]);
+#endif
     if constexpr (NEXT) {
       chol_publish<MT>(L, cc, K1);
+#ifdef GST_EXP_NOPIV  // timing experiment only: pivot chain cut
+      nxt.akk = 2.0;
+#else
       nxt.akk = rdlane(L[SL(K1, K1)], 9 * KK1);
+#endif
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       chol_load<MT, K1, KK1>(cc, nxt);
-      nxt.sk = rcp_nr1(nxt.akk);
+      pivot_rcp<MT>(nxt);
     }
   }
-  // off the critical path: capture pivot / aug entry (lane k % 64) and the rest of the
-  // trailing update; log|Sigma|, the quad form and the failure flag are reduced from these
-  // lane-parallel after the elimination (chol_stats), not accumulated per step
-  cc.apr[k / 64] = (cc.lane == (k & 63)) ? cur.akk : cc.apr[k / 64];
-  cc.zr[k / 64] = (cc.lane == (k & 63)) ? cur.zk : cc.zr[k / 64];
+  // lrs = a_ik / a_kk for the rest of the trailing update (one multiply per row, then one
+  // FMA per element)
+  const double sk = fma(cur.y0, cur.e, cur.y0);
+  double lrs[MT];
+#pragma unroll
+  for (int r = K; r < MT; ++r) lrs[r] = cur.lr[r] * sk;
+  // off the critical path: the rest of the trailing update
 #pragma unroll
   for (int s = K; s < MT; ++s) {
     if (s == K1 || (KK == 7 && s == K)) continue;  // slot column K is done when KK == 7
@@ -374,7 +400,7 @@ __device__ __forceinline__ void chol_range(double (&L)[SL(MT, 0)], CholCtx& cc) 
   c.akk = rdlane(L[SL(KLO, KLO)], 0);
   lds_order();
   chol_load<MT, KLO, 0>(cc, c);
-  c.sk = rcp_nr1(c.akk);
+  pivot_rcp<MT>(c);
   chol_step<MT, KLO, 0, KEND>(L, cc, c);
   lds_order();
 }
@@ -384,6 +410,35 @@ __device__ __forceinline__ void chol_range(double (&L)[SL(MT, 0)], CholCtx& cc) 
 // product + exponent sum (log taken once by the caller), sum a_{raug,k}^2 / a_kk and the
 // failure flag, all wave-uniform.  Branch-free on purpose: a lane-divergent region here,
 // inside the register-critical hyper block, makes the allocator spill ~1.4 KB per lane.
+__device__ __forceinline__ double bperm(double v, int src_lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_bpermute(4 * src_lane, (int)(b & 0xffffffffll));
+  const int hi = __builtin_amdgcn_ds_bpermute(4 * src_lane, (int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// After an elimination over columns [KLO, KEND): the pivot of column j = 8K+q is frozen in
+// lane (q,q) slot (K,K) and its augmented-row entry in lane (RA%8, q) slot (RA/8, K); lane
+// j % 64 of apr / zr[j / 64] fetches both (one lane permute per slot column, no branch).
+template <int MT, int KLO, int KEND, int RA>
+__device__ __forceinline__ void chol_harvest(const double (&L)[SL(MT, 0)], CholCtx& cc) {
+  constexpr int R = RA / 8, PA = RA % 8;
+  static_assert(KEND <= RA && RA < 8 * MT, "augmented row below the eliminated columns");
+#pragma unroll
+  for (int K = KLO / 8; K <= (KEND - 1) / 8; ++K) {
+    const double vd = bperm(L[SL(K, K)], 9 * cc.q);
+    const double vz = bperm(L[SL(R, K)], 8 * PA + cc.q);
+    const int j = 8 * K + cc.q;
+    const bool in = (j >= KLO) && (j < KEND);
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      const bool mine = in && (8 * sl + cc.p == K);
+      cc.apr[sl] = mine ? vd : cc.apr[sl];
+      cc.zr[sl] = mine ? vz : cc.zr[sl];
+    }
+  }
+}
+
 template <int KLO, int KEND>
 __device__ __forceinline__ void chol_stats(CholCtx& cc) {
   double mm = 1.0, qd = 0.0;
@@ -742,6 +797,7 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
     CholCtx cc{colq, lane, p, q, raug, 1.0, 0.0, 0, 0, {1.0, 1.0}, {0.0, 0.0}};
     GST_SUB_END(10)
     chol_range<MT, 0, 8 * K0>(L, cc);
+    chol_harvest<MT, 0, 8 * K0, RA>(L, cc);
     chol_stats<0, 8 * K0>(cc);
     GST_SUB_END(11)
     tm_apr = cc.apr[0];
@@ -780,6 +836,7 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
     CholCtx cc{colq, lane, p, q, raug, 1.0, 0.0, 0, 0, {tm_apr, 1.0}, {tm_zr, 0.0}};
     GST_SUB_END(7)
     chol_range<MT, K0, RA>(L, cc);
+    chol_harvest<MT, 8 * K0, RA, RA>(L, cc);
     chol_stats<8 * K0, RA>(cc);
     GST_SUB_END(8)
     f_apr[0] = cc.apr[0];
