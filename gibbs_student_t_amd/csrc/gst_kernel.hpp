@@ -1137,17 +1137,21 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
         for (int r = 0; r < MT; ++r) vr[r] = 0.0;
 #pragma unroll
         for (int K = MT - 1; K >= 0; --K) {
+          // rows of the slots below K are solved: their part of every column 8K+q is one
+          // per-lane sum, formed once per slot; each column step then adds only its
+          // in-slot rows (vr[K] is zero for rows not yet solved)
+          double pe = 0.0, po2 = 0.0;
+#pragma unroll
+          for (int r = K + 1; r < MT; r += 2) {
+            pe = fma(L[SL(r, K)], vr[r], pe);
+            if (r + 1 < MT) po2 = fma(L[SL(r + 1, K)], vr[r + 1], po2);
+          }
+          const double below = pe + po2;
 #pragma unroll 1
           for (int kk = 7; kk >= 0; --kk) {
             const int k = 8 * K + kk;
             if (k >= raug) continue;
-            double pe = 0.0, po2 = 0.0;
-#pragma unroll
-            for (int r = K; r < MT; r += 2) {
-              pe = fma(L[SL(r, K)], vr[r], pe);
-              if (r + 1 < MT) po2 = fma(L[SL(r + 1, K)], vr[r + 1], po2);
-            }
-            const double sk = col_sum(pe + po2, kk);
+            const double sk = col_sum(fma(L[SL(K, K)], vr[K], below), kk);
             const double yk = yinv[k];
             const double vk = (wvec[k] - yk * sk) * yk;
             vr[K] = (p == kk) ? vk : vr[K];
