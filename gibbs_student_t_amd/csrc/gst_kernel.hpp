@@ -1138,25 +1138,40 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
 #pragma unroll
         for (int K = MT - 1; K >= 0; --K) {
           // rows of the slots below K are solved: their part of every column 8K+q is one
-          // per-lane sum, formed once per slot; each column step then adds only its
-          // in-slot rows (vr[K] is zero for rows not yet solved)
+          // per-lane sum, reduced over p once per slot column (every lane (p, q) gets the
+          // sum of column 8K+q); the 8 in-slot columns are then solved with uniform values
           double pe = 0.0, po2 = 0.0;
 #pragma unroll
           for (int r = K + 1; r < MT; r += 2) {
             pe = fma(L[SL(r, K)], vr[r], pe);
             if (r + 1 < MT) po2 = fma(L[SL(r + 1, K)], vr[r + 1], po2);
           }
-          const double below = pe + po2;
-#pragma unroll 1
+          double acc = pe + po2;
+          acc += dpp<DPP_ROR8>(acc);  // (l + 8) mod 16 == l ^ 8: p and p ^ 1
+          acc += __shfl_xor(acc, 16, 64);
+          acc += __shfl_xor(acc, 32, 64);
+          // diagonal block, transposed through LDS: dcol[i] = a_{8K+i, 8K+q}
+          tbuf[8 * q + p] = L[SL(K, K)];
+          lds_order();
+          double dcol[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) dcol[i] = tbuf[8 * q + i];
+          const int kq = 8 * K + q;
+          const double wq = wvec[kq], yq = yinv[kq];
+          lds_order();
+          double vmine = 0.0;
+#pragma unroll
           for (int kk = 7; kk >= 0; --kk) {
-            const int k = 8 * K + kk;
-            if (k >= raug) continue;
-            const double sk = col_sum(fma(L[SL(K, K)], vr[K], below), kk);
-            const double yk = yinv[k];
-            const double vk = (wvec[k] - yk * sk) * yk;
-            vr[K] = (p == kk) ? vk : vr[K];
-            xbuf[k] = vk;
+            if (8 * K + kk >= raug) continue;
+            // lanes q == kk now hold sum_{i>k} a_ik v_i of column k = 8K + kk
+            const double vq = (wq - yq * acc) * yq;
+            const double vk = rdlane(vq, kk);
+            vmine = (q == kk) ? vk : vmine;
+            acc = fma(dcol[kk], vk, acc);  // row k's term of the columns q < kk
           }
+          xbuf[kq] = vmine;  // zero for the pad columns k >= raug
+          lds_order();
+          vr[K] = xbuf[8 * K + p];
         }
         lds_order();
         GST_SUB_END(13)
