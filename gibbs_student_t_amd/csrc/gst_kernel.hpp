@@ -31,13 +31,15 @@ namespace gst {
 
 typedef double v4d __attribute__((ext_vector_type(4)));
 
+__host__ __device__ constexpr int CQ(int MT) { return 8 * MT + ((4 - 8 * MT) % 32 + 32) % 32; }
+
 // waves (chains) per workgroup: as many as the per-wave LDS footprint allows (one
 // workgroup per CU at these sizes; never more than 4 = one wave per SIMD)
 __host__ __device__ constexpr int wpb_for(int MT, int NS) {
 #ifdef GST_WPB_OVERRIDE  // diagnostic builds only (per-CU contention experiments)
   return GST_WPB_OVERRIDE;
 #endif
-  return (8 * (8 * MT + 2) + 16 * 17 + 64 * NS + 7 * 8 * MT + 32 + 128 +
+  return (8 * CQ(MT) + 16 * 17 + 64 * NS + 9 * 8 * MT + 32 + 128 +
           64 * ((MT - 2) * (MT - 1) / 2)) * 8 * 4 <= 160 * 1024
              ? 4
              : 2;
@@ -103,7 +105,7 @@ __host__ __device__ constexpr int SL(int r, int s) { return r * (r + 1) / 2 + s;
 // different; measured, round 1), with ds_write_b64 they are exact.  Per-q stride CQ = 8*MT rounded up to 4 mod 32 doubles: with the
 // row stride MT = 10, the 16 lanes (p in {0,1}, q in 0..7) of a publishing ds_write_b128
 // then cover 16 distinct 16-byte bank groups.
-__host__ __device__ constexpr int CQ(int MT) { return 8 * MT + ((4 - 8 * MT) % 32 + 32) % 32; }
+// (CQ: see the published-column buffers below)
 
 #ifdef GST_STAMPS
 #define GST_STAMP_DECL \
@@ -477,7 +479,7 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
   constexpr int NS0 = SL(MT - K0, 0);  // S0 slots (r >= s >= K0)
   constexpr int TB_LD = 17;
   constexpr int WPB = wpb_for(MT, NS);
-  constexpr int LDSW = 8 * CQ(MT) + 16 * TB_LD + 64 * NS + 7 * MP + 32 + 4 * 32;
+  constexpr int LDSW = 8 * CQ(MT) + 16 * TB_LD + 64 * NS + 9 * MP + 32 + 4 * 32;
   __shared__ double smem[WPB][LDSW];
   __shared__ double s0mem[WPB][NS0 * 64];   // Schur complement S0, [slot][lane]
 
@@ -509,6 +511,8 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
   double* yinv = xbuf + MP;           // 1/sqrt(a_kk)
   double* dfbuf = yinv + MP;          // 32
   double* mhv = dfbuf + 32;           // [30][4] MH variates: u_scale, index, jump, log(u_acc)
+  double* lfq = mhv + 4 * 32;         // log f_k of the power law (copy of md.lfreq)
+  double* ldq = lfq + MP;             // log df_k (copy of md.ldf)
   double* S0 = s0mem[wv] + lane;      // S0[64 * slot]
 
   static_assert(RA >= 8 * K0 + 1 && RA < 8 * MT, "augmented row out of range");
@@ -532,6 +536,10 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
   double nu = st.nu[c];
   for (int j = lane; j < MP; j += 64) bbuf[j] = (j < m) ? st.b[(size_t)c * m + j] : 0.0;
   for (int j = lane; j < MP; j += 64) phbuf[j] = 0.0;
+  for (int j = lane; j < md.nf; j += 64) {
+    lfq[j] = md.lfreq[j];
+    ldq[j] = md.ldf[j];
+  }
 
   double rr[NS], s2[NS], al[NS], po[NS], yv[NS];
   int cls[NS];
@@ -820,7 +828,7 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
     // log phi_k = 2 lA ln10 - log(12 pi^2) + (g-3) log fyr - g log f_k + log df_k
     const double lc = 2.0 * lA * 2.302585092994045684 - md.log_12pi2 + (g - 3.0) * md.log_fyr;
     for (int f = lane; f < md.nf; f += 64)
-      phbuf[md.ntm_pad + f] = exp(-(lc - g * md.lfreq[f] + md.ldf[f]));
+      phbuf[md.ntm_pad + f] = exp(-(lc - g * lfq[f] + ldq[f]));
     // sum_k log phi_k in closed form (no reduction on the critical path)
     const double logdet_phi =
         ((double)md.nf * lc - g * md.sum_lfreq + md.sum_ldf) + md.logdet_phi_tm;
