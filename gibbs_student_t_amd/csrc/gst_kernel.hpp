@@ -753,28 +753,36 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
 #pragma unroll
     for (int i = 0; i < NTT; ++i) acc[i] = (v4d){0.0, 0.0, 0.0, 0.0};
     const int tl = lane >> 4;
-    double tv[NT], tn[NT];
+    // two k-steps in flight: each operand set is reloaded (for k-step ks + 2) right after
+    // its MFMAs have issued, so a T load has two k-steps (30 MFMAs) to arrive from L2
+    double ta[NT], tb[NT];
+    auto tload = [&](double (&t)[NT], int ks) __attribute__((always_inline)) {
+      const double* src = md.Tmf + (size_t)ks * NT * 64 + lane;
 #pragma unroll
-    for (int X = 0; X < NT; ++X) tv[X] = md.Tmf[X * 64 + lane];
-#pragma unroll 1
-    for (int ks = 0; ks < md.nks; ++ks) {
-      if (ks + 1 < md.nks) {
-        const double* src = md.Tmf + (size_t)(ks + 1) * NT * 64 + lane;
-#pragma unroll
-        for (int X = 0; X < NT; ++X) tn[X] = src[X * 64];
-      }
+      for (int X = 0; X < NT; ++X) t[X] = src[X * 64];
+    };
+    auto kstep = [&](const double (&t)[NT], int ks) __attribute__((always_inline)) {
       const double wt = vbuf[4 * ks + tl];
 #pragma unroll
       for (int I = 0; I < NT; ++I) {
-        const double av = tv[I] * wt;
+        const double av = t[I] * wt;
 #pragma unroll
         for (int J = 0; J <= I; ++J) {
           acc[I * (I + 1) / 2 + J] =
-              __builtin_amdgcn_mfma_f64_16x16x4f64(av, tv[J], acc[I * (I + 1) / 2 + J], 0, 0, 0);
+              __builtin_amdgcn_mfma_f64_16x16x4f64(av, t[J], acc[I * (I + 1) / 2 + J], 0, 0, 0);
         }
       }
-#pragma unroll
-      for (int X = 0; X < NT; ++X) tv[X] = tn[X];
+    };
+    tload(ta, 0);
+    if (md.nks > 1) tload(tb, 1);
+#pragma unroll 1
+    for (int ks = 0; ks < md.nks; ks += 2) {
+      kstep(ta, ks);
+      if (ks + 2 < md.nks) tload(ta, ks + 2);
+      if (ks + 1 < md.nks) {
+        kstep(tb, ks + 1);
+        if (ks + 3 < md.nks) tload(tb, ks + 3);
+      }
     }
     GST_SUB_END(9)
     // MFMA C layout (col = lane&15, row = lane>>4 + 4 reg) -> cyclic register layout
