@@ -755,14 +755,14 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
     const int tl = lane >> 4;
     // two k-steps in flight: each operand set is reloaded (for k-step ks + 2) right after
     // its MFMAs have issued, so a T load has two k-steps (30 MFMAs) to arrive from L2
-    double ta[NT], tb[NT];
-    auto tload = [&](double (&t)[NT], int ks) __attribute__((always_inline)) {
+    double ta[NT], tb[NT], wa, wb;
+    auto tload = [&](double (&t)[NT], double& w, int ks) __attribute__((always_inline)) {
       const double* src = md.Tmf + (size_t)ks * NT * 64 + lane;
 #pragma unroll
       for (int X = 0; X < NT; ++X) t[X] = src[X * 64];
+      w = vbuf[4 * ks + tl];
     };
-    auto kstep = [&](const double (&t)[NT], int ks) __attribute__((always_inline)) {
-      const double wt = vbuf[4 * ks + tl];
+    auto kstep = [&](const double (&t)[NT], const double wt) __attribute__((always_inline)) {
 #pragma unroll
       for (int I = 0; I < NT; ++I) {
         const double av = t[I] * wt;
@@ -773,15 +773,15 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
         }
       }
     };
-    tload(ta, 0);
-    if (md.nks > 1) tload(tb, 1);
+    tload(ta, wa, 0);
+    if (md.nks > 1) tload(tb, wb, 1);
 #pragma unroll 1
     for (int ks = 0; ks < md.nks; ks += 2) {
-      kstep(ta, ks);
-      if (ks + 2 < md.nks) tload(ta, ks + 2);
+      kstep(ta, wa);
+      if (ks + 2 < md.nks) tload(ta, wa, ks + 2);
       if (ks + 1 < md.nks) {
-        kstep(tb, ks + 1);
-        if (ks + 3 < md.nks) tload(tb, ks + 3);
+        kstep(tb, wb);
+        if (ks + 3 < md.nks) tload(tb, wb, ks + 3);
       }
     }
     GST_SUB_END(9)
