@@ -39,6 +39,7 @@ struct Ctx {
   gst::DevModel* dmd = nullptr;    // device array [nd] (in allocs)
   int nd = 0, nmax = 0, m = 0, raug = 0;
   int MT = 0, NS = 0, K0 = 0, WPB = 4;
+  int ncu = 256;                   // compute units of the device (workgroup sizing)
   int path_req = GST_PATH_AUTO;    // gst_set_path
   int path = GST_PATH_PERSISTENT;  // chosen by gst_model_set
   std::vector<void*> allocs;
@@ -84,17 +85,23 @@ typedef void (*kfn_t)(const gst::DevModel*, const gst::DevState, const gst::DevR
                       const gst::DevTape, int, int, long long, int, unsigned,
                       unsigned long long, long long, int, double*, double*);
 
-template <int MT, int NS, int K0, int RA, bool TAPE>
+template <int MT, int NS, int K0, int RA, bool TAPE, int WPB = gst::wpb_for(MT, NS)>
 kfn_t kfn() {
-  return &gst::gst_sweep_kernel<MT, NS, K0, RA, TAPE>;
+  return &gst::gst_sweep_kernel<MT, NS, K0, RA, TAPE, WPB>;
 }
 
 // Instantiated shapes: MT = padded matrix dim / 8, NS = TOA slots of 64, K0 = timing-model
 // panels of 8, RA = augmented-row index = 8*K0 + nfourier (the elimination length).
-kfn_t pick(int MT, int NS, int K0, int RA, bool tape) {
-#define GST_CASE(mt, ns, k0, ra)                                          \
-  if (MT == mt && NS == ns && K0 == k0 && RA == ra)                       \
-    return tape ? kfn<mt, ns, k0, ra, true>() : kfn<mt, ns, k0, ra, false>();
+// wpb: chains per workgroup (the default, wpb_for, or 2 / 1 for sampling launches with
+// fewer chains than fill every SIMD; tape-mode parity launches always use the default).
+kfn_t pick(int MT, int NS, int K0, int RA, bool tape, int wpb) {
+#define GST_CASE(mt, ns, k0, ra)                                                  \
+  if (MT == mt && NS == ns && K0 == k0 && RA == ra) {                             \
+    if (tape) return kfn<mt, ns, k0, ra, true>();                                 \
+    if (wpb == 1) return kfn<mt, ns, k0, ra, false, 1>();                         \
+    if (wpb == 2) return kfn<mt, ns, k0, ra, false, 2>();                         \
+    return kfn<mt, ns, k0, ra, false>();                                          \
+  }
   GST_CASE(10, 2, 2, 76)   // J1713-like, n <= 128 (no_outlier datasets)
   GST_CASE(10, 3, 2, 76)   // J1713+0747: n = 130, 30 red-noise components, 14 TM columns
   GST_CASE(10, 4, 2, 76)   // n <= 256
@@ -126,6 +133,9 @@ int gst_ctx_create(int device, void** ctx) {
   HIP_OK(hipSetDevice(device));
   Ctx* cx = new Ctx();
   cx->device = device;
+  hipDeviceProp_t prop;
+  HIP_OK(hipGetDeviceProperties(&prop, device));
+  cx->ncu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   HIP_OK(hipEventCreate(&cx->ev0));
   HIP_OK(hipEventCreate(&cx->ev1));
   *ctx = cx;
@@ -358,7 +368,7 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
   const int MT = mpad / 8, K0 = ntm_pad / 8;
   const int nsl = (nmax + 63) / 64;
   const int NS = nsl <= 2 ? 2 : (nsl <= 3 ? 3 : 4);
-  const bool fits = round_up(nmax, 4) <= 64 * NS && pick(MT, NS, K0, raug, false);
+  const bool fits = round_up(nmax, 4) <= 64 * NS && pick(MT, NS, K0, raug, false, 4);
   int path = cx->path_req;
   if (path == GST_PATH_AUTO) path = fits ? GST_PATH_PERSISTENT : GST_PATH_LARGE;
   if (path == GST_PATH_PERSISTENT && !fits) {
@@ -540,9 +550,15 @@ static int launch(Ctx* cx, const gst_state* s, const gst_records* r, const gst_t
   if (cx->path == GST_PATH_LARGE)
     return launch_large(cx, ds, dr, dt, C, nsweeps, sweep0, record_every, mask, seed, chain0,
                         eval_only, ow, oh, (hipStream_t)stream);
-  kfn_t k = pick(cx->MT, cx->NS, cx->K0, cx->raug, tape);
+  // chains per workgroup: the fewest (1, 2, default) that still fit one workgroup per CU
+  int wpb = cx->WPB;
+  if (!tape) {
+    if (wpb >= 1 && C <= cx->ncu) wpb = 1;
+    else if (wpb >= 2 && C <= 2 * cx->ncu) wpb = 2;
+  }
+  kfn_t k = pick(cx->MT, cx->NS, cx->K0, cx->raug, tape, wpb);
   if (!k) return fail("gst: no kernel instance");
-  const dim3 grid((C + cx->WPB - 1) / cx->WPB), block(64 * cx->WPB);
+  const dim3 grid((C + wpb - 1) / wpb), block(64 * wpb);
   hipStream_t st = (hipStream_t)stream;
   HIP_OK(hipEventRecord(cx->ev0, st));
   hipLaunchKernelGGL(k, grid, block, 0, st, cx->dmd, ds, dr, dt, C, nsweeps, sweep0,

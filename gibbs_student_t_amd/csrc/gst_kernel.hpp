@@ -466,8 +466,11 @@ __device__ __forceinline__ void chol_stats(CholCtx& cc) {
   cc.fail = __ballot(f) != 0ull ? 1 : 0;
 }
 
-template <int MT, int NS, int K0, int RA, bool TAPE>
-__global__ void __launch_bounds__(64 * wpb_for(MT, NS))
+// WPB = chains (waves) per workgroup: wpb_for(MT, NS) fills a CU with one chain per SIMD;
+// the host picks fewer when the launch has fewer chains than 4 x CUs, so the chains spread
+// over every CU instead of sharing the LDS of a quarter of them.
+template <int MT, int NS, int K0, int RA, bool TAPE, int WPB = wpb_for(MT, NS)>
+__global__ void __launch_bounds__(64 * WPB)
     gst_sweep_kernel(const DevModel* __restrict__ mds, const DevState st, const DevRec rec, const DevTape tape,
                      int C, int nsweeps, long long sweep0, int record_every, unsigned mask,
                      unsigned long long seed, long long chain0, int eval_only, double* out_w,
@@ -478,7 +481,7 @@ __global__ void __launch_bounds__(64 * wpb_for(MT, NS))
   constexpr int MP = 8 * MT;
   constexpr int NS0 = SL(MT - K0, 0);  // S0 slots (r >= s >= K0)
   constexpr int TB_LD = 17;
-  constexpr int WPB = wpb_for(MT, NS);
+  static_assert(WPB >= 1 && WPB <= wpb_for(MT, NS), "workgroup exceeds the LDS budget");
   constexpr int LDSW = 8 * CQ(MT) + 16 * TB_LD + 64 * NS + 9 * MP + 32 + 4 * 32;
   __shared__ double smem[WPB][LDSW];
   __shared__ double s0mem[WPB][NS0 * 64];   // Schur complement S0, [slot][lane]
