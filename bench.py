@@ -1,21 +1,33 @@
 """Benchmark: aggregate Gibbs sweeps/s (+ ESS/s) on J1713+0747, batched chains per GPU.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--chains C] [--config 2|3|4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--chains C] [--config 2|3|4|5]
 
-A *step* is one Gibbs sweep (gibbs.py:354-380) of every chain on every rank.  Each rank
-owns C chains (weak scaling, default 1024 = BASELINE config 2 per GPU) of the run_sims.py
-'beta' outlier-mixture model (run_sims.py:98-99) on J1713+0747's 130 TOAs; the timed region
-is exactly K sweeps in one persistent launch, recording every sweep's full state (chain,
-bchain, zchain, alphachain, poutchain, thetachain, dfchain) to HBM as the reference records
-every sweep.  For N > 1 the driver starts one process per GPU with torch.distributed.run;
-chains never communicate while sampling, the only collective is the final summary
-all-reduce (RCCL).  Rank 0 prints one JSON line.
+A *step* is one Gibbs sweep (gibbs.py:354-380) of every chain on every rank.  Each rank owns
+C chains (weak scaling; default 2048 per GPU = two chains per SIMD, the "1024+" of the
+BASELINE metric) of the run_sims.py 'beta' outlier-mixture model (run_sims.py:98-99) on
+J1713+0747's 130 TOAs.  The timed region is exactly K sweeps in one persistent launch,
+recording every sweep's full state (chain, bchain, zchain, alphachain, poutchain,
+thetachain, dfchain) to HBM as the reference records every sweep.
+
+Multi-GPU: one process per GPU.  Under torch.distributed.run the ranks come from the
+environment; launched plainly with ``--gpus N > 1`` this script is the launcher: it starts
+N rank processes itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, 127.0.0.1) before
+anything touches a GPU and relays rank 0's JSON line.  Chains never communicate while
+sampling; the collectives are the final all-gather of every chain's post-burn-in draws
+(global split-R-hat and bulk-ESS over ALL chains) and a max-reduce of the timings.
+
+ESS/s has its own window, independent of --steps: after the timed region every chain
+runs ``--ess-burn`` more sweeps (discarded), then ``--ess-window`` recorded sweeps of the
+sampled parameters and theta, timed on their own; ESS/s = min over quantities of the
+bulk-ESS summed over datasets / window seconds, reported only when every global R-hat is
+<= 1.01 (else null, with the reason).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
@@ -29,66 +41,38 @@ METRIC = "Gibbs sweeps/sec (node aggregate) + ESS/sec, J1713+0747, 1/2/4/8 GPU"
 FP64_PEAK_TFLOPS = 78.6      # MI355X fp64 matrix (= vector) dense peak, AMD spec
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 CFG = dict(model="mixture", vary_df=True, theta_prior="beta")   # run_sims.py:98-99
+RHAT_OK = 1.01
+CONFIG4_DATASETS = 256
 
 
-def algorithmic_flops(n: int, m: int) -> float:
+def algorithmic_flops(n: float, m: int) -> float:
     """Fixed work per chain-sweep: Gram of [T|r], 12 Cholesky (11 MH + 1
     draw), 12 pairs of triangular solves, one T b."""
     return n * (m + 1) * (m + 2) + 12 * m ** 3 / 3 + 12 * 4 * m ** 2 + 2 * n * m
 
 
-def toa_pass_bytes(n: int) -> float:
+def executed_flops(n: float, nf: int, ntm: int, m: int) -> dict:
+    """Flops the Schur-complement algorithm actually performs per chain-sweep:
+    the Gram once, the timing-model columns eliminated once, the 11 hyper likelihoods each
+    factor only the (nf + 1)-row Fourier block (+ augmented row), the b draw's two solves
+    and T b.  Reported next to the fixed formula (SURVEY.md 8d asks for both)."""
+    M = ntm + nf + 1                      # system rows incl. the augmented residual row
+    gram = n * (m + 1) * (m + 2)
+    tm = sum((M - 1 - k) * (M - k) for k in range(ntm))
+    hyper = 11 * sum((nf - k) * (nf + 1 - k) for k in range(nf))
+    solves = 4 * m * m
+    tb = 2 * n * m
+    return {"gram": gram, "tm_elim": tm, "hyper_chol": hyper, "b_solves": solves, "tb": tb,
+            "total": gram + tm + hyper + solves + tb}
+
+
+def toa_pass_bytes(n: float) -> float:
     """Per-TOA pass HBM bytes per chain-sweep: 8 n (6 + 2*21)."""
     return 8.0 * n * (6 + 2 * 21)
 
 
 # ------------------------------------------------------------------------------------------
-# CPU baseline: the oracle (a faithful port of gibbs.py, bit-exact to the reference on the
-# same MT19937 stream) timed on host cores, one chain per single-threaded process.
-# ------------------------------------------------------------------------------------------
-def _cpu_worker(seconds: float, seed: int):
-    import warnings
-
-    from gibbs_student_t_amd import data
-    from gibbs_student_t_amd.model import PTA
-    from oracle.gibbs_oracle import (LegacyNumpyVariates, Oracle, OutlierModel,
-                                     initial_state)
-    warnings.simplefilter("ignore")
-    pta = PTA(data.j1713())
-    orc = Oracle(pta, OutlierModel(**CFG))
-    np.random.seed(seed)
-    x = pta.sample_params()
-    st = initial_state(pta, orc.cfg)
-    src = LegacyNumpyVariates()
-    for _ in range(3):
-        x = orc.sweep(st, x, src)
-    t0 = time.perf_counter()
-    k = 0
-    while time.perf_counter() - t0 < seconds:
-        x = orc.sweep(st, x, src)
-        k += 1
-    print(json.dumps({"sweeps": k, "seconds": time.perf_counter() - t0}))
-
-
-def cpu_baseline(seconds: float, cores: int):
-    env = dict(os.environ, OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1",
-               MKL_NUM_THREADS="1", HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
-    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker",
-                               str(seconds), str(1000 + i)], env=env, stdout=subprocess.PIPE,
-                              stderr=subprocess.DEVNULL, text=True) for i in range(cores)]
-    tot = 0.0
-    sweeps = 0
-    for p in procs:
-        out, _ = p.communicate(timeout=seconds * 10 + 120)
-        r = json.loads(out.strip().splitlines()[-1])
-        tot += r["sweeps"] / r["seconds"]
-        sweeps += r["sweeps"]
-    return {"value": tot, "unit": "chain-sweeps/s", "cores": cores, "kind": "port",
-            "sample": f"{cores} single-thread processes x {seconds:.0f} s of the oracle "
-                      f"(oracle/gibbs_oracle.py, numpy legacy RNG, bit-exact to gibbs.py), "
-                      f"one J1713 mixture chain each, {sweeps} sweeps total"}
-
-
+# workloads (BASELINE.json configs)
 # ------------------------------------------------------------------------------------------
 def initial_state(pta, C: int, chain0: int):
     """Prior draws per global chain id (run_sims.py:111) and the gibbs.py:29-51 latents."""
@@ -100,45 +84,67 @@ def initial_state(pta, C: int, chain0: int):
                 pout=np.zeros((C, n)), theta=np.full(C, 0.01), nu=np.full(C, 4.0))
 
 
-def workload(config: int, rank: int, world: int, chains: int | None):
-    """BASELINE.json configs as (datasets, cfgs, chain->dataset, initial state, description).
-
-    2: J1713+0747 epochs, 1024 chains per GPU (the headline, default);
-    3: simulate_data.py pulsar, 5% outliers, red.txt red noise, 512 chains per GPU
-       (4096 over 8 GPUs);
-    4: run_sims.py grid, 256 datasets (3 outlier fractions x {Gaussian, Student-t nu=4}
-       white noise x outlier/no_outlier twins x 5 outlier models) x 64 chains, 32
-       datasets per GPU.
-    All weak scaling: the per-GPU work is fixed as the GPU count grows.
-    """
-    from gibbs_student_t_amd import data
-    from gibbs_student_t_amd import run_sims
+def config_datasets(config: int):
+    """(ptas, cfgs) of a config's whole job, in global order (no sharding)."""
+    from gibbs_student_t_amd import data, run_sims
     from gibbs_student_t_amd.model import PTA
-    if config in (2, 3):
-        if config == 2:
-            pta = PTA(data.j1713())
-            C = chains or 1024
-            desc = ("J1713+0747 Student-t/outlier-mixture Gibbs sampler (run_sims 'beta' "
-                    "model), fp64")
-            dat = ("synthetic residuals at the 130 real J1713+0747 TOA epochs (white + "
-                   "power-law red + 5% outliers, seeded); chains start from prior draws")
-        else:
-            out, _ = data.simulate_data(seed=2017, theta=0.05, red_source="red.txt")
-            pta = PTA(out)
-            C = chains or 512
-            desc = ("simulate_data.py pulsar (J1713+0747 epochs, log-normal errors, red.txt "
-                    "red noise, 5% outliers), run_sims 'beta' model, fp64")
-            dat = ("simulate_data.py restatement: log-normal error bars, the reference's "
-                   "red.txt realisation, Bernoulli(0.05) outliers with sigma_out = 1 us")
+    if config == 2:
+        return [PTA(data.j1713())], [CFG]
+    if config == 3:
+        out, _ = data.simulate_data(seed=2017, theta=0.05, red_source="red.txt")
+        return [PTA(out)], [CFG]
+    if config == 4:
+        grid = run_sims.build_grid(thetas=(0.05, 0.1, 0.15), realisations=5,
+                                   dofs=(None, 4.0))[:CONFIG4_DATASETS]
+        return [e.pta for e in grid], [e.cfg for e in grid]
+    if config == 5:
+        psr = data.scaled_synthetic(n=100_000, components=60, ntm=300, seed=5)
+        return [PTA(psr, components=60)], [CFG]
+    raise SystemExit(f"unknown --config {config}")
+
+
+def workload(config: int, rank: int, world: int, chains: int | None):
+    """This rank's share of a BASELINE.json config.
+
+    2: J1713+0747 epochs, 2048 chains per GPU (weak scaling; the headline, default);
+    3: simulate_data.py pulsar, 5% outliers, red.txt red noise, 512 chains per GPU
+       (4096 over 8 GPUs; weak scaling);
+    4: run_sims.py grid: 256 datasets (3 outlier fractions x {Gaussian, Student-t nu=4}
+       white noise x outlier/no_outlier twins x 5 outlier models) x 64 chains, the
+       datasets sharded over the GPUs (strong scaling: 256 / N datasets per GPU);
+    5: scaled synthetic, 100k TOAs, m = 420, 512 chains per GPU (large-model path).
+    """
+    from gibbs_student_t_amd import run_sims
+    if config in (2, 3, 5):
+        ptas, cfgs = config_datasets(config)
+        C = chains or {2: 2048, 3: 512, 5: 512}[config]
         c0 = rank * C
-        return dict(ptas=[pta], cfgs=[CFG], ds=np.zeros(C, np.int32),
-                    init=initial_state(pta, C, c0), chain0=c0, C=C, desc=desc, data=dat,
-                    per=C)
+        desc = {
+            2: "J1713+0747 Student-t/outlier-mixture Gibbs sampler (run_sims 'beta' model), fp64",
+            3: "simulate_data.py pulsar (J1713+0747 epochs, log-normal errors, red.txt red "
+               "noise, 5% outliers), run_sims 'beta' model, fp64",
+            5: "scaled synthetic pulsar: 100k TOAs over 10 yr, 60 red-noise components (120 "
+               "Fourier columns) + 300 timing/DMX columns (m=420), run_sims 'beta' model, "
+               "512 chains per GPU, fp64, large-model path"}[config]
+        dat = {
+            2: "synthetic residuals at the 130 real J1713+0747 TOA epochs (white + power-law "
+               "red + 5% outliers, seeded); chains start from prior draws",
+            3: "simulate_data.py restatement: log-normal error bars, the reference's red.txt "
+               "realisation, Bernoulli(0.05) outliers with sigma_out = 1 us",
+            5: "data.scaled_synthetic: log-normal error bars, power-law red noise, 5% "
+               "outliers, random 300-column timing/DMX design matrix projected out; records "
+               "x, b, theta, nu every sweep (per-TOA chains not recorded: 1.2 GB per sweep)"}[config]
+        return dict(ptas=ptas, cfgs=cfgs, ds=np.zeros(C, np.int32),
+                    init=initial_state(ptas[0], C, c0), chain0=c0, C=C, desc=desc, data=dat,
+                    per=C, dsid=np.zeros(C, np.int64), scaling="weak")
     if config == 4:
         per_entry = chains or 64
         grid = run_sims.build_grid(thetas=(0.05, 0.1, 0.15), realisations=5,
-                                   dofs=(None, 4.0))[:256]
-        per_rank = 256 // 8 if world <= 8 else max(1, 256 // world)
+                                   dofs=(None, 4.0))[:CONFIG4_DATASETS]
+        if CONFIG4_DATASETS % world:
+            raise SystemExit(f"config 4 shards {CONFIG4_DATASETS} datasets: --gpus must "
+                             f"divide it")
+        per_rank = CONFIG4_DATASETS // world
         e0 = rank * per_rank
         mine = grid[e0:e0 + per_rank]
         nst = max(e.pta.n for e in mine)
@@ -146,28 +152,181 @@ def workload(config: int, rank: int, world: int, chains: int | None):
                  for i, e in enumerate(mine)]
         init = {k: np.concatenate([p_[k] for p_ in parts]) for k in parts[0]}
         C = len(mine) * per_entry
-        return dict(ptas=[e.pta for e in mine], cfgs=[e.cfg for e in mine],
-                    ds=np.repeat(np.arange(len(mine)), per_entry).astype(np.int32), init=init,
-                    chain0=e0 * per_entry, C=C, per=per_entry,
-                    desc=("run_sims.py grid: 256 simulated datasets (theta 0.05/0.1/0.15, "
-                          "Gaussian and Student-t nu=4 white noise, outlier + no_outlier "
-                          "twins, 5 outlier models) x 64 chains, 32 datasets per GPU, fp64"),
-                    data="simulate_data.py restatement per dataset (seeded), ragged n")
-    if config == 5:
-        psr = data.scaled_synthetic(n=100_000, components=60, ntm=300, seed=5)
-        pta = PTA(psr, components=60)
-        C = chains or 512
-        c0 = rank * C
-        return dict(ptas=[pta], cfgs=[CFG], ds=np.zeros(C, np.int32),
-                    init=initial_state(pta, C, c0), chain0=c0, C=C, per=C,
-                    desc=("scaled synthetic pulsar: 100k TOAs over 10 yr, 60 red-noise "
-                          "components (120 Fourier columns) + 300 timing/DMX columns (m=420), "
-                          "run_sims 'beta' model, 512 chains per GPU, fp64, large-model path"),
-                    data=("data.scaled_synthetic: log-normal error bars, power-law red noise, "
-                          "5% outliers, random 300-column timing/DMX design matrix projected "
-                          "out; records x, b, theta, nu every sweep (per-TOA chains not "
-                          "recorded: 1.2 GB per sweep)"))
+        ds = np.repeat(np.arange(len(mine)), per_entry).astype(np.int32)
+        return dict(ptas=[e.pta for e in mine], cfgs=[e.cfg for e in mine], ds=ds, init=init,
+                    chain0=e0 * per_entry, C=C, per=per_entry, dsid=(e0 + ds).astype(np.int64),
+                    desc=(f"run_sims.py grid: {CONFIG4_DATASETS} simulated datasets (theta "
+                          "0.05/0.1/0.15, Gaussian and Student-t nu=4 white noise, outlier + "
+                          "no_outlier twins, 5 outlier models) x 64 chains, datasets sharded "
+                          "over the GPUs, fp64"),
+                    data="simulate_data.py restatement per dataset (seeded), ragged n",
+                    scaling="strong")
     raise SystemExit(f"unknown --config {config}")
+
+
+# ------------------------------------------------------------------------------------------
+# CPU baseline: the oracle (a faithful port of gibbs.py, bit-exact to the reference on the
+# same MT19937 stream) timed on host cores, one chain per single-threaded process, on the
+# same workload as --config.
+# ------------------------------------------------------------------------------------------
+def _cpu_worker(config: int, seconds: float, seed: int, slot: int):
+    import warnings
+
+    from oracle.gibbs_oracle import (LegacyNumpyVariates, Oracle, OutlierModel,
+                                     initial_state as orc_init)
+    warnings.simplefilter("ignore")
+    ptas, cfgs = config_datasets(config)
+    k = slot % len(ptas)                      # config 4: the processes cycle the grid
+    pta, cfg = ptas[k], cfgs[k]
+    orc = Oracle(pta, OutlierModel(**cfg))
+    np.random.seed(seed)
+    x = pta.sample_params()
+    st = orc_init(pta, orc.cfg)
+    src = LegacyNumpyVariates()
+    x = orc.sweep(st, x, src)
+    t0 = time.perf_counter()
+    k = 0
+    while time.perf_counter() - t0 < seconds:
+        x = orc.sweep(st, x, src)
+        k += 1
+    print(json.dumps({"sweeps": k, "seconds": time.perf_counter() - t0}))
+
+
+def cpu_baseline(config: int, seconds: float, cores: int):
+    env = dict(os.environ, OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1",
+               MKL_NUM_THREADS="1", HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker",
+                               str(config), str(seconds), str(1000 + i), str(i)], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+             for i in range(cores)]
+    tot, sweeps = 0.0, 0
+    for p in procs:
+        out, _ = p.communicate(timeout=seconds * 10 + 300)
+        r = json.loads(out.strip().splitlines()[-1])
+        tot += r["sweeps"] / r["seconds"]
+        sweeps += r["sweeps"]
+    what = {2: "one J1713 mixture chain each", 3: "one config-3 (red.txt) mixture chain each",
+            4: "each a chain of a different run_sims grid dataset/model",
+            5: "one 100k-TOA m=420 mixture chain each"}[config]
+    return {"value": tot, "unit": "chain-sweeps/s", "cores": cores, "kind": "port",
+            "sample": f"config {config}: {cores} single-thread processes x {seconds:.0f} s of "
+                      f"the oracle (oracle/gibbs_oracle.py, numpy legacy RNG, bit-exact to "
+                      f"gibbs.py), {what}, {sweeps} sweeps total"}
+
+
+# ------------------------------------------------------------------------------------------
+# launcher: --gpus N without torch.distributed.run -> N rank processes (never touches a GPU)
+# ------------------------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv: list[str]) -> int:
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env, stdout=subprocess.PIPE if r == 0 else None,
+                                      text=True))
+    out, _ = procs[0].communicate()
+    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+    sys.stdout.write(out)
+    sys.stdout.flush()
+    return max(abs(rc) for rc in rcs)
+
+
+# ------------------------------------------------------------------------------------------
+# CPU stand-in of the sampler (--stub): lets the launcher, the sharding and the global
+# diagnostics be tested on a machine without a GPU.  Each chain is an AR(1) series keyed
+# by (seed, global chain id, sweep), so draws do not depend on the sharding.
+# ------------------------------------------------------------------------------------------
+class StubSampler:
+    path = "stub"
+    RHO = 0.6
+
+    def __init__(self, ptas, cfgs, device=0):
+        import torch
+        self.P = len(ptas[0].params)
+        self.n, self.m = int(max(p.T.shape[0] for p in ptas)), int(ptas[0].T.shape[1])
+        self.tdev = torch.device("cpu")
+
+    def alloc(self, C, dataset=None):
+        self.C = int(C)
+        self.x = np.zeros((self.C, self.P))
+        self.theta = np.zeros(self.C)
+
+    def set_state(self, x=None, theta=None, **_):
+        if x is not None:
+            self.x[:] = x
+        if theta is not None:
+            self.theta[:] = theta
+
+    def alloc_records(self, nrec, keys=("x",)):
+        import torch
+        shapes = {"x": (self.P,), "theta": ()}
+        return {k: torch.zeros((self.C, nrec) + shapes.get(k, (1,)), dtype=torch.float64)
+                for k in keys}
+
+    def sweep(self, nsweeps, records=None, seed=0, sweep0=0, chain0=0, **_):
+        import torch
+        r = self.RHO
+        for it in range(nsweeps):
+            for c in range(self.C):
+                rng = np.random.default_rng([seed, chain0 + c, sweep0 + it])
+                if records is not None:
+                    if "x" in records:
+                        records["x"][c, it] = torch.from_numpy(self.x[c])
+                    if "theta" in records:
+                        records["theta"][c, it] = float(self.theta[c])
+                e = rng.standard_normal(self.P + 1)
+                self.x[c] = r * self.x[c] + np.sqrt(1 - r * r) * e[:self.P]
+                self.theta[c] = r * self.theta[c] + np.sqrt(1 - r * r) * e[self.P]
+        self._ms = 1e-3 * nsweeps
+
+    def last_kernel_ms(self):
+        return self._ms
+
+    def get_state(self):
+        return {"status": np.zeros(self.C, np.int32)}
+
+    def set_timing(self, on):
+        pass
+
+    def kernel_times(self):
+        return {}
+
+    def close(self):
+        pass
+
+
+# ------------------------------------------------------------------------------------------
+def global_diagnostics(draws: np.ndarray, theta: np.ndarray, dsid: np.ndarray,
+                       names: list[str], theta_on: np.ndarray):
+    """Split-R-hat and bulk-ESS over ALL gathered chains.  ``draws`` [C, S, P], ``theta``
+    [C, S], ``dsid`` [C] (dataset of each chain: chains of one dataset share a posterior),
+    ``theta_on`` [ndatasets] (theta is updated by the dataset's model).  ESS is summed over
+    datasets, R-hat maximised over them."""
+    from gibbs_student_t_amd import diag
+    keys = names + ["theta"]
+    ess = {k: 0.0 for k in keys}
+    rhat = {k: 0.0 for k in keys}
+    for d in np.unique(dsid):
+        sel = dsid == d
+        series = {nm: draws[sel, :, j] for j, nm in enumerate(names)}
+        if theta_on[d]:
+            series["theta"] = theta[sel]
+        for k, v in series.items():
+            e = diag.bulk_ess(v)
+            ess[k] += e if np.isfinite(e) else 0.0
+            r = diag.split_rhat(v)
+            rhat[k] = max(rhat[k], r if np.isfinite(r) else np.inf)
+    return ess, rhat
 
 
 def main():
@@ -176,36 +335,55 @@ def main():
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5),
-                    help="BASELINE.json config (2 = headline J1713+0747, 1024 chains/GPU)")
+                    help="BASELINE.json config (2 = headline J1713+0747)")
     ap.add_argument("--chains", type=int, default=None,
                     help="chains per GPU (config 4: per dataset)")
     ap.add_argument("--seed", type=int, default=20171713)
+    ap.add_argument("--ess-burn", type=int, default=None,
+                    help="extra discarded sweeps before the ESS window (default 3000; "
+                         "config 5: no ESS window)")
+    ap.add_argument("--ess-window", type=int, default=None,
+                    help="recorded sweeps of the ESS window (default 1000; config 5: 0)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-worker", nargs=2, default=None)
+    ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-worker", nargs=4, default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.cpu_worker:
-        _cpu_worker(float(args.cpu_worker[0]), int(args.cpu_worker[1]))
-        return
+        _cpu_worker(int(args.cpu_worker[0]), float(args.cpu_worker[1]),
+                    int(args.cpu_worker[2]), int(args.cpu_worker[3]))
+        return 0
 
     from gibbs_student_t_amd import dist
     rank, local, world = dist.env_rank()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus, sys.argv[1:])     # before anything touches a GPU
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cores = max(1, min(16, os.cpu_count() or 1))
-        cpu = cpu_baseline(args.cpu_seconds, cores)      # before the GPU is touched
+    if world == 1 and not args.no_cpu_baseline and not args.stub:
+        cores = max(1, min(16 if args.config != 5 else 8, os.cpu_count() or 1))
+        secs = args.cpu_seconds if args.config != 5 else max(args.cpu_seconds, 20.0)
+        cpu = cpu_baseline(args.config, secs, cores)      # before the GPU is touched
+    ess_burn = args.ess_burn if args.ess_burn is not None else (0 if args.config == 5 else 3000)
+    ess_win = args.ess_window if args.ess_window is not None else (0 if args.config == 5 else 1000)
 
     import torch
-    from gibbs_student_t_amd import diag
-    from gibbs_student_t_amd.native import NativeSampler
+    rank, local, world = dist.init("gloo" if args.stub else None)
+    if args.stub:
+        dev, Sampler = None, StubSampler
 
-    rank, local, world = dist.init()
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+        def sync():
+            pass
+    else:
+        from gibbs_student_t_amd.native import NativeSampler as Sampler
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+
+        def sync():
+            torch.cuda.synchronize(dev)
     wl = workload(args.config, rank, world, args.chains)
     C, K, W = wl["C"], args.steps, args.warmup
     c0 = wl["chain0"]
-    ns = NativeSampler(wl["ptas"], wl["cfgs"], local)
+    ns = Sampler(wl["ptas"], wl["cfgs"], local)
     ns.alloc(C, dataset=wl["ds"])
     ns.set_state(**wl["init"])
     if W > 0:
@@ -215,54 +393,64 @@ def main():
                            ("x", "b", "z", "alpha", "pout", "theta", "nu"))
     if large:
         ns.set_timing(True)
-    torch.cuda.synchronize(dev)
-    dist.barrier(dev)
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    ns.sweep(K, records=rec, seed=args.seed, sweep0=W, chain0=c0)
-    torch.cuda.synchronize(dev)
-    dist.barrier(dev)
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
+
+    def timed(fn):
+        sync()
+        dist.barrier(dev)
+        sync()
+        t0 = time.perf_counter()
+        fn()
+        sync()
+        dist.barrier(dev)
+        sync()
+        return time.perf_counter() - t0
+
+    # ---- the timed region: exactly K sweeps, every sweep recorded
+    elapsed = timed(lambda: ns.sweep(K, records=rec, seed=args.seed, sweep0=W, chain0=c0))
     kernel_ms = ns.last_kernel_ms()
     ktimes = ns.kernel_times() if large else None
     status = ns.get_state()["status"]
+    del rec
+    if large:
+        ns.set_timing(False)
 
-    # ESS per dataset (its chains share one posterior), summed over datasets and ranks
-    xs = rec["x"].cpu().numpy()
-    th = rec["theta"].cpu().numpy()
+    # ---- ESS window: its own burn-in (discarded) and recorded window, timed on its own
     names = [p.name.split("_", 1)[1] for p in wl["ptas"][0].params]
-    keys = names + ["theta"]
-    ess = {k: 0.0 for k in keys}
-    rhat = {k: 0.0 for k in keys}
-    for d in range(len(wl["ptas"])):
-        sel = wl["ds"] == d
-        series = {nm: xs[sel, :, j] for j, nm in enumerate(names)}
-        series["theta"] = th[sel]
-        for k, v in series.items():
-            if k == "theta" and wl["cfgs"][d]["model"] not in ("mixture", "vvh17"):
-                continue            # theta is never updated: no ESS to speak of
-            e = diag.bulk_ess(v)
-            ess[k] += e if np.isfinite(e) else 0.0
-            r = diag.split_rhat(v)
-            rhat[k] = max(rhat[k], r if np.isfinite(r) else 0.0)
-    s_vec = np.array([ess[k] for k in keys] + [float((status != 0).sum())])
-    m_vec = np.array([elapsed, kernel_ms] + [rhat[k] for k in keys])
+    ess = rhat = None
+    win_s = 0.0
+    if ess_win > 0:
+        if ess_burn > 0:
+            ns.sweep(ess_burn, seed=args.seed, sweep0=W + K, chain0=c0)
+        wrec = ns.alloc_records(ess_win, keys=("x", "theta"))
+        win_s = timed(lambda: ns.sweep(ess_win, records=wrec, seed=args.seed,
+                                       sweep0=W + K + ess_burn, chain0=c0))
+        draws = dist.gather_chains(torch.cat([wrec["x"], wrec["theta"][..., None]], dim=2)
+                                   .cpu().numpy(), dev)
+        dsid = dist.gather_chains(wl["dsid"].astype(np.float64), dev).astype(np.int64)
+        if rank == 0:
+            _, allcfgs = config_datasets(args.config) if args.config == 4 else (None, wl["cfgs"])
+            theta_on = np.array([c["model"] in ("mixture", "vvh17") for c in allcfgs])
+            ess, rhat = global_diagnostics(draws[..., :-1], draws[..., -1], dsid, names,
+                                           theta_on)
+        del wrec, draws
+    shards = dist.gather_chains(np.array([[c0, c0 + C]], dtype=np.float64), dev)
+    m_vec = np.array([elapsed, kernel_ms, win_s])
+    s_vec = np.array([float((status != 0).sum())])
     s_vec, m_vec = dist.reduce_summary(s_vec, m_vec, dev)
-    elapsed, kernel_ms = float(m_vec[0]), float(m_vec[1])
-    ess_tot = dict(zip(keys, s_vec[:len(keys)]))
-    rhat_max = dict(zip(keys, m_vec[2:]))
+    elapsed, kernel_ms, win_s = (float(v) for v in m_vec)
 
     if rank == 0:
         total = C * world * K
         value = total / elapsed
         n_mean = float(np.mean([p_.T.shape[0] for p_ in wl["ptas"]]))
-        n, m = wl["ptas"][0].T.shape
+        pta0 = wl["ptas"][0]
+        n, m = pta0.T.shape
         n_eff = n if args.config != 4 else n_mean
         flops = algorithmic_flops(n_eff, m) * C * K
         achieved = flops / (kernel_ms * 1e-3) / 1e12
+        exe = executed_flops(n_eff, pta0.nfourier, pta0.ntm, m)
         stages = None
-        toa_ms = kernel_ms
+        toa = None
         if ktimes:
             # dominant kernel = the Gram; its algorithmic flops per launch are the
             # n (m+1) (m+2) term of the fixed formula x chains (one launch per sweep)
@@ -271,11 +459,16 @@ def main():
             achieved = gram_flop / (g_ms / g_n * 1e-3) / 1e12
             stages = {k: {"ms_per_sweep": v[0] / max(1, K), "launches": v[1]}
                       for k, v in ktimes.items()}
-            # per-TOA pass (white MH rescans + theta/z/alpha/nu) over its own kernels' time
+            # the per-TOA pass is its own kernels here (white MH rescans + theta/z/alpha/nu),
+            # timed per launch by HIP events
             toa_ms = ktimes["white"][0] + ktimes["toa"][0]
+            gbs = toa_pass_bytes(n_eff) * C * K / (toa_ms * 1e-3) / 1e9
+            toa = {"kernels": "lg_white + lg_toa (HIP events per launch)", "GBps": gbs,
+                   "hbm_frac": gbs / HBM_PEAK_GBS,
+                   "bytes_per_chain_sweep": toa_pass_bytes(n_eff)}
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc) and args.config == 2:
+        if os.path.exists(pmc) and args.config == 2 and not args.stub:
             try:
                 pj = json.load(open(pmc))
                 traffic = pj["hbm_bytes_per_chain_sweep"] * C * K
@@ -288,8 +481,17 @@ def main():
                 traffic = g["hbm_read_bytes"] + g["hbm_write_bytes"]
             except Exception:
                 traffic = None
-        pos = [v for v in ess_tot.values() if v > 0]
-        min_ess = float(min(pos)) if pos else None
+        ess_ps, reason = None, None
+        if ess is None:
+            reason = "no ESS window (config 5: 155 ms per sweep)" if ess_win <= 0 else "n/a"
+        else:
+            bad = {k: v for k, v in rhat.items() if not v <= RHAT_OK and ess.get(k, 0) > 0}
+            pos = [v for v in ess.values() if v > 0]
+            if bad:
+                reason = f"R-hat > {RHAT_OK} after the window's burn-in: {bad}"
+            elif pos and win_s > 0:
+                # ESS over every chain of the job / the window's wall time (max over ranks)
+                ess_ps = float(min(pos)) / win_s
         out = {
             "metric": METRIC,
             "value": value,
@@ -299,7 +501,7 @@ def main():
             "warmup": W,
             "ms_per_step": elapsed / K * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": wl["scaling"],
             "vs_baseline": None,
             "dtype": "f64",
             "data": wl["data"],
@@ -308,21 +510,25 @@ def main():
                        "basis_cols": m, "datasets_per_gpu": len(wl["ptas"]),
                        "record_every": 1,
                        "parallelism": f"independent chains sharded over {world} GPU(s); "
-                                      "RCCL only for the final summary all-reduce"},
-            "ess_per_sec": (min_ess / elapsed) if min_ess else None,
-            "ess_total": {k: float(v) for k, v in ess_tot.items()},
-            "rhat_max": {k: float(v) for k, v in rhat_max.items()},
-            "chains_with_status": int(s_vec[-1]),
+                                      "RCCL only for the final all-gather of chain draws"},
+            "ess_per_sec": ess_ps,
+            "ess_per_sec_reason": reason,
+            "ess_window": {"burn_in_sweeps": W + K + ess_burn, "sweeps": ess_win,
+                           "seconds": win_s, "chains": C * world,
+                           "ess_total": ess, "rhat_max": rhat},
+            "shards": [[int(a), int(b)] for a, b in shards],   # global chain ids per rank
+            "chains_with_status": int(s_vec[0]),
             "kernel_ms": kernel_ms,
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
                          "traffic": traffic,
                          "kernel": "lg_gram (per-launch HIP events)" if large else
-                                   "gst_sweep_kernel (persistent, whole launch)",
+                                   "gst_sweep_kernel (persistent, whole launch, HIP events)",
                          "algorithmic_flop_per_chain_sweep": algorithmic_flops(n_eff, m),
-                         "toa_pass_GBps": toa_pass_bytes(n_eff) * C * K / (toa_ms * 1e-3) / 1e9,
-                         "toa_pass_hbm_frac": toa_pass_bytes(n_eff) * C * K / (toa_ms * 1e-3)
-                         / 1e9 / HBM_PEAK_GBS},
+                         "executed_flop_per_chain_sweep": exe,
+                         "per_toa_pass": toa if toa else
+                         "fused into the persistent kernel (no separate launch to time); "
+                         "stage shares in profiles/r2_stages_config2.txt"},
             "cpu_baseline": cpu,
         }
         if stages:
@@ -330,7 +536,8 @@ def main():
         print(json.dumps(out), flush=True)
     ns.close()
     dist.finalize()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

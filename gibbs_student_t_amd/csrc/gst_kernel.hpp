@@ -1084,7 +1084,9 @@ __global__ void __launch_bounds__(64 * WPB)
         if (step < 0) {
           l0 = l1;
           p0 = p1;
-          Lvalid = true;
+          // a failed initial factorisation is no factor to draw b from: if every proposal
+          // is then skipped, step NHYPER refactors (and flags status 2) instead
+          Lvalid = !f1;
           if (eval_only) {
             if (lane == 0) out_h[c] = l1;
             break;

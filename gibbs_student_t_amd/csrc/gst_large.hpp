@@ -664,7 +664,9 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
       if (step < 0) {
         l0 = l1;
         p0 = p1;
-        Lvalid = true;
+        // a failed initial factorisation is no factor to draw b from: if every proposal
+        // is then skipped, step NHYPER refactors (and flags status 2) instead
+        Lvalid = !f1;
         if (a.eval_only) {
           if (tid == 0) a.out_h[c] = l1;
           break;

@@ -100,27 +100,46 @@ def simulate_residuals(toas, toaerrs, U, *, theta=0.05, sigma_out=1e-6, log10_A=
     return r, z
 
 
-def j1713(seed: int = 1713, theta: float = 0.05, sigma_out: float = 1e-6,
-          red_source: str = "powerlaw") -> PulsarData:
-    """J1713+0747 at its 130 real epochs with synthetic residuals (configs 1-2).
+def at_epochs(raw: dict, seed: int = 1713, theta: float = 0.05, sigma_out: float = 1e-6,
+              red_source: str = "powerlaw", name: str = "PSR") -> PulsarData:
+    """A pulsar at the epochs / error bars / timing model of ``raw`` (``load_j1713_raw`` or
+    ``partim.load_raw`` layout) with synthetic residuals (simulate_data.py:10-39 recipe).
 
-    ``red_source='red.txt'`` adds the reference's precomputed red-noise realisation
-    (red.txt, interpreted in days as libstempo perturbs ``stoas``) instead
+    ``red_source='red.txt'`` adds ``raw['red']`` (the reference's precomputed red-noise
+    realisation, interpreted in days as libstempo perturbs ``stoas``) instead
     of a fresh power-law draw.
     """
-    raw = load_j1713_raw()
     mjd = raw["mjd_int"].astype(np.float64) + raw["mjd_frac"]
     toas = mjd * DAY_SEC
     toaerrs = raw["toaerr_us"] * 1e-6
     M = design_matrix(mjd, raw["par"], raw["fit"])
     U = np.linalg.svd(M, full_matrices=False)[0]
     rng = np.random.default_rng(seed)
-    red = raw["red"] * DAY_SEC if red_source == "red.txt" else None
+    red = None
+    if red_source == "red.txt":
+        if raw.get("red") is None or len(raw["red"]) != len(mjd):
+            raise ValueError("red_source='red.txt' needs one red-noise value per TOA")
+        red = raw["red"] * DAY_SEC
     r, z = simulate_residuals(toas, toaerrs, U, theta=theta, sigma_out=sigma_out,
                               rng=rng, red=red)
-    return PulsarData(name="J1713+0747", toas=toas, residuals=r, toaerrs=toaerrs, Mmat=M,
+    return PulsarData(name=name, toas=toas, residuals=r, toaerrs=toaerrs, Mmat=M,
                       freqs=raw["freq_mhz"], meta={"z_true": z, "seed": seed,
                                                    "theta": theta})
+
+
+def j1713(seed: int = 1713, theta: float = 0.05, sigma_out: float = 1e-6,
+          red_source: str = "powerlaw") -> PulsarData:
+    """J1713+0747 at its 130 real epochs with synthetic residuals (configs 1-2)."""
+    return at_epochs(load_j1713_raw(), seed, theta, sigma_out, red_source, "J1713+0747")
+
+
+def load_partim(par: str, tim: str, red: str | None = None, **kw) -> PulsarData:
+    """Any pulsar's tempo2 par/tim pair (gibbs_student_t_amd.partim) at its own epochs,
+    error bars and fitted timing model, with synthetic residuals as in ``at_epochs``
+    (tempo2 residuals are unavailable offline: parity unpinned)."""
+    from . import partim
+    raw = partim.load_raw(par, tim, red)
+    return at_epochs(raw, name=raw["name"] or "PSR", **kw)
 
 
 def simulate_data(seed: int, theta: float = 0.05, sigma_out: float = 1e-6,
@@ -179,5 +198,5 @@ def scaled_synthetic(n: int = 100_000, components: int = 60, ntm: int = 300, see
                       meta={"z_true": z, "seed": seed, "theta": theta})
 
 
-__all__ = ["load_j1713_raw", "scaled_synthetic", "design_matrix", "simulate_residuals", "j1713", "simulate_data",
-           "FYR"]
+__all__ = ["load_j1713_raw", "scaled_synthetic", "design_matrix", "simulate_residuals", "j1713",
+           "at_epochs", "load_partim", "simulate_data", "FYR"]

@@ -51,6 +51,25 @@ def reduce_summary(vec_sum: np.ndarray, vec_max: np.ndarray, device=None):
     return s.cpu().numpy(), m.cpu().numpy()
 
 
+def gather_chains(arr: np.ndarray, device=None) -> np.ndarray:
+    """All-gather per-chain arrays (leading axis = this rank's chains, same shape on
+    every rank) in rank order, i.e. global chain order: the one data collective of a run
+    (SURVEY.md 8e), so R-hat / ESS are computed over ALL chains, not per rank.  On GPU
+    ranks the tensors travel over RCCL (xGMI); one ~C x draws x params fp64 block per rank,
+    once per run."""
+    import torch
+    import torch.distributed as dist
+    a = np.ascontiguousarray(arr, dtype=np.float64)
+    if not (dist.is_available() and dist.is_initialized()):
+        return a
+    world = dist.get_world_size()
+    dev = device if device is not None else torch.device("cpu")
+    t = torch.as_tensor(a, device=dev)
+    out = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+    dist.all_gather_into_tensor(out, t)
+    return out.cpu().numpy()
+
+
 def barrier(device=None):
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized():

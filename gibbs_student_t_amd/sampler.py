@@ -6,6 +6,8 @@ chain arrays gain a leading chain axis when > 1), ``seed`` (Philox key), ``devic
 ``record_every`` (thin the chain arrays) and ``chunk`` (sweeps per kernel launch).
 
 Differences from the reference, all documented in DESIGN.md:
+* ``update_b`` recomputes T^T N^-1 T from the current state; the reference reuses whatever
+  TNT/d its last likelihood call cached (gibbs.py:159-161);
 * variates come from on-device Philox4x32-10 instead of numpy's MT19937 stream, so chains
   are distributionally -- not bitwise -- equal to the reference's for the same seed;
 * the b draw uses the Cholesky square root (mean = cho_solve(Sigma, d), the reference's own
@@ -63,29 +65,26 @@ class Gibbs:
     def _view(self, a):
         return a[0] if self.nchains == 1 else a
 
-    @property
-    def _b(self):
-        return self._view(self._b_all)
+    def _assign(self, name, value):
+        a = getattr(self, name)
+        v = np.asarray(value, dtype=np.float64)
+        if self.nchains == 1:
+            a[0] = v
+        else:
+            a[...] = v
 
-    @property
-    def _z(self):
-        return self._view(self._z_all)
-
-    @property
-    def _alpha(self):
-        return self._view(self._alpha_all)
-
-    @property
-    def _pout(self):
-        return self._view(self._pout_all)
-
-    @property
-    def _theta(self):
-        return self._theta_all[0] if self.nchains == 1 else self._theta_all
-
-    @property
-    def tdf(self):
-        return self._tdf_all[0] if self.nchains == 1 else self._tdf_all
+    _b = property(lambda self: self._view(self._b_all),
+                  lambda self, v: self._assign("_b_all", v))
+    _z = property(lambda self: self._view(self._z_all),
+                  lambda self, v: self._assign("_z_all", v))
+    _alpha = property(lambda self: self._view(self._alpha_all),
+                      lambda self, v: self._assign("_alpha_all", v))
+    _pout = property(lambda self: self._view(self._pout_all),
+                     lambda self, v: self._assign("_pout_all", v))
+    _theta = property(lambda self: self._theta_all[0] if self.nchains == 1 else self._theta_all,
+                      lambda self, v: self._assign("_theta_all", v))
+    tdf = property(lambda self: self._tdf_all[0] if self.nchains == 1 else self._tdf_all,
+                   lambda self, v: self._assign("_tdf_all", v))
 
     # ---- parameter helpers (gibbs.py:53-77) ----------------------------------------------
     @property
@@ -109,11 +108,12 @@ class Gibbs:
         return sum(p.get_logpdf(x) for p, x in zip(self.params, xs))
 
     def get_lnlikelihood_df(self, df):
-        """gibbs.py:331-335 (host: a 30-point scalar function)."""
+        """gibbs.py:331-335 (host: a 30-point scalar function); one value per chain."""
         n = len(self._residuals)
-        a = self._alpha_all[0]
-        return -(df / 2) * np.sum(np.log(a) + 1 / a) + n * (df / 2) * np.log(df / 2) \
+        a = self._alpha_all
+        v = -(df / 2) * np.sum(np.log(a) + 1 / a, axis=1) + n * (df / 2) * np.log(df / 2) \
             - n * scipy.special.gammaln(df / 2)
+        return v[0] if self.nchains == 1 else v
 
     def _xs_all(self, xs):
         xs = np.asarray(xs, dtype=np.float64)
@@ -146,44 +146,46 @@ class Gibbs:
         return self._lnlikes(xs)[1]
 
     # ---- single-stage updates (each one GPU launch with a stage mask) -----------------------
+    # As in the reference (gibbs.py:80-259) a stage method RETURNS its draw and leaves the
+    # latent state (_b, _theta, _z, _alpha, tdf) alone; only update_z records _pout
+    # (gibbs.py:225).  Callers commit, e.g. ``g._b = g.update_b(x)`` (gibbs.py:374-380).
+    # Each call advances the Philox sweep counter, so repeated calls draw afresh.
     def _stage(self, xs, mask):
         self._push(self._xs_all(xs))
         self._native.sweep(1, mask=mask, seed=self.seed, sweep0=self._sweep_counter)
         self._sweep_counter += 1
-        x = self._pull()
-        return x[0] if self.nchains == 1 else x
+        s = self._native.get_state()
+        self.status = s["status"]
+        return s
+
+    def _ret(self, a):
+        return a[0] if self.nchains == 1 else a
 
     def update_white_params(self, xs):
-        return self._stage(xs, _abi.STAGE_WHITE)
+        return self._ret(self._stage(xs, _abi.STAGE_WHITE)["x"])
 
     def update_hyper_params(self, xs):
-        return self._stage(xs, _abi.STAGE_HYPER)
+        return self._ret(self._stage(xs, _abi.STAGE_HYPER)["x"])
 
     def update_b(self, xs):
         # a direct call draws unconditionally (gibbs.py:145-182); the :373 test belongs to
         # sample() only
-        self._push(self._xs_all(xs))
-        self._native.sweep(1, mask=_abi.STAGE_B | _abi.STAGE_B_FORCE, seed=self.seed,
-                           sweep0=self._sweep_counter)
-        self._sweep_counter += 1
-        self._pull()
-        return self._b
+        return self._ret(self._stage(xs, _abi.STAGE_B | _abi.STAGE_B_FORCE)["b"])
 
     def update_theta(self, xs):
-        self._stage(xs, _abi.STAGE_THETA)
-        return self._theta
+        return self._ret(self._stage(xs, _abi.STAGE_THETA)["theta"])
 
     def update_z(self, xs):
-        self._stage(xs, _abi.STAGE_Z)
-        return self._z
+        s = self._stage(xs, _abi.STAGE_Z)
+        if self._lmodel in ("mixture", "vvh17"):
+            self._pout_all = s["pout"]                       # gibbs.py:225
+        return self._ret(s["z"])
 
     def update_alpha(self, xs):
-        self._stage(xs, _abi.STAGE_ALPHA)
-        return self._alpha
+        return self._ret(self._stage(xs, _abi.STAGE_ALPHA)["alpha"])
 
     def update_df(self, xs):
-        self._stage(xs, _abi.STAGE_DF)
-        return self.tdf
+        return self._ret(self._stage(xs, _abi.STAGE_DF)["nu"])
 
     # ---- the sampler (gibbs.py:342-385) ----------------------------------------------------
     def sample(self, xs, niter=10000):

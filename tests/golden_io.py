@@ -11,6 +11,9 @@ from gibbs_student_t_amd.model import PTA
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
+# fixture-name prefix -> tests/golden/{prefix}_dataset.npz (tools/gen_golden.py)
+DATASETS = ("sim", "twob", "simclean", "scaled", "c3", "c4t")
+
 CHAIN_KEYS = ("chain", "bchain", "zchain", "poutchain", "thetachain", "alphachain", "dfchain")
 
 
@@ -30,7 +33,7 @@ def load_ref(name):
     d = dict(np.load(os.path.join(GOLDEN, f"ref_{name}.npz"), allow_pickle=False))
     d["kw"] = ast.literal_eval(str(d.pop("model_kw")))
     d["tape"] = {k[5:]: v for k, v in d.items() if k.startswith("tape_")}
-    ds = name.split("_")[0] if name.split("_")[0] in ("sim", "twob", "simclean", "scaled") else "j1713"
+    ds = name.split("_")[0] if name.split("_")[0] in DATASETS else "j1713"
     d["pta"] = load_dataset(efac="efac" in name, dataset=ds)
     return d
 
@@ -49,3 +52,31 @@ def sweep_state(ref, i):
 
 def sweep_tape(ref, i):
     return {k: v[i] for k, v in ref["tape"].items()}
+
+
+def oracle_chol_replay(ref, S=None):
+    """The oracle replaying the reference's tape for S sweeps from the recorded start with
+    the Cholesky mean and the recorded draw term (b = cho_solve(Sigma, d) + b_delta,
+    gibbs.py:321-322 + 169-180).  That is the expression the HIP path evaluates in tape
+    mode, so the two chains agree to fp64 rounding, not to the SVD-vs-Cholesky mean gap
+    that separates both from the reference's own chain.  Returns records {key: [S, ...]}
+    of the state at the start of each sweep (gibbs.py:355-361)."""
+    import warnings
+
+    from oracle.gibbs_oracle import ChainState, Oracle, OutlierModel, TapeVariates
+    S = int(ref["niter"]) if S is None else int(S)
+    orc = Oracle(ref["pta"], OutlierModel(**ref["kw"]))
+    s0 = sweep_state(ref, 0)
+    st = ChainState(b=s0["b"].copy(), z=s0["z"].copy(), alpha=s0["alpha"].copy(),
+                    pout=s0["pout"].copy(), theta=s0["theta"], nu=s0["nu"])
+    x = np.array(ref["xs"], dtype=np.float64)
+    rec = {k: [] for k in ("x", "b", "z", "alpha", "pout", "theta", "nu")}
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for i in range(S):
+            for k, v in (("x", x), ("b", st.b), ("z", np.asarray(st.z, float)),
+                         ("alpha", st.alpha), ("pout", st.pout), ("theta", st.theta),
+                         ("nu", float(st.nu))):
+                rec[k].append(np.array(v, dtype=np.float64, copy=True))
+            x = orc.sweep(st, x, TapeVariates(sweep_tape(ref, i)), b_mean="chol_delta")
+    return {k: np.stack(v) for k, v in rec.items()}

@@ -1,0 +1,47 @@
+"""bench.py's multi-GPU path on CPU: the --gpus N launcher, sharding and global diagnostics.
+
+``--stub`` swaps the HIP sampler for a CPU AR(1) stand-in keyed by (seed, global chain id,
+sweep) -- the same keying as the device Philox streams -- so a 2-rank run over gloo must
+produce the same global R-hat / ESS as one process holding all the chains.
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*args):
+    env = dict(os.environ)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--stub",
+                          "--steps", "6", "--warmup", "2", "--ess-burn", "4",
+                          "--ess-window", "60", *args], env=env, capture_output=True,
+                         text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    return json.loads(lines[0])
+
+
+def test_two_rank_launch_matches_one_process():
+    two = _run("--gpus", "2", "--chains", "6")
+    one = _run("--gpus", "1", "--chains", "12")
+    assert two["n_gpus"] == 2 and one["n_gpus"] == 1
+    assert two["config"]["chains_total"] == one["config"]["chains_total"] == 12
+    assert two["shards"] == [[0, 6], [6, 12]] and one["shards"] == [[0, 12]]
+    # global diagnostics over ALL chains: identical draws -> identical R-hat and ESS
+    w2, w1 = two["ess_window"], one["ess_window"]
+    assert w2["chains"] == w1["chains"] == 12
+    for k in w1["rhat_max"]:
+        assert w2["rhat_max"][k] == w1["rhat_max"][k]
+        assert w2["ess_total"][k] == w1["ess_total"][k]
+    assert two["cpu_baseline"] is None
+
+
+def test_launcher_reports_world_size_four():
+    four = _run("--gpus", "4", "--chains", "3")
+    assert four["n_gpus"] == 4 and four["config"]["chains_total"] == 12
+    assert [s[0] for s in four["shards"]] == [0, 3, 6, 9]

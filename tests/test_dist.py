@@ -84,7 +84,7 @@ def _workload_worker(rank, world, port, out):
 
 def test_two_rank_bench_workloads_partition_chains():
     """bench.py under torch.distributed.run: ranks own disjoint global chain ids (Philox
-    keys) and agree on the data; config 4 shards the run_sims grid by dataset."""
+    keys) and agree on the data; config 4 shards the 256-dataset run_sims grid by dataset (strong scaling)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -104,4 +104,4 @@ def test_two_rank_bench_workloads_partition_chains():
     assert len(set(ck2)) == 1
     ent4, C4 = res[0][4][3], res[0][4][2]
     assert set(ent4[:C4]).isdisjoint(set(ent4[C4:]))          # run_sims entries sharded
-    assert sorted(set(ent4)) == list(range(64))               # 32 per rank, 64 chains each
+    assert sorted(set(ent4)) == list(range(256))              # 128 per rank, 64 chains each

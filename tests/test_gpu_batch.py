@@ -10,7 +10,7 @@ identical to a launch of its dataset alone.
 import numpy as np
 import pytest
 
-from golden_io import fixture_names, load_ref, sweep_state
+from golden_io import fixture_names, load_ref, oracle_chol_replay, sweep_state
 
 pytestmark = pytest.mark.gpu
 
@@ -19,6 +19,7 @@ if not torch.cuda.is_available():  # pragma: no cover
     pytest.skip("needs a HIP device", allow_module_level=True)
 
 from gibbs_student_t_amd.native import NativeSampler, pack_tape  # noqa: E402
+from test_gpu_parity import assert_replay_matches  # noqa: E402
 
 # three-parameter fixtures the single-chain replay covers (test_full_chain_replay), plus the
 # ragged no_outlier twin (n = 119 next to n = 130)
@@ -58,6 +59,10 @@ def test_batch_replays_every_fixture():
     assert np.all(ns.get_state()["status"] == 0)
     for c, (name, r) in enumerate(zip(REPLAY, refs)):
         n = r["pta"].n
+        # 1e-10 against the oracle's Cholesky-mean replay of the same tape ...
+        assert_replay_matches({k: v[c] for k, v in got.items()}, oracle_chol_replay(r, S), r,
+                              name)
+        # ... and the reference's own (SVD-mean) chain, whose mean error compounds
         np.testing.assert_array_equal(got["x"][c], r["chain"], err_msg=name)
         np.testing.assert_array_equal(got["z"][c][:, :n], r["zchain"], err_msg=name)
         np.testing.assert_array_equal(got["nu"][c], r["dfchain"], err_msg=name)

@@ -1,0 +1,104 @@
+"""BASELINE configs 3 and 4 at their own shapes on the GPU (Philox mode, property checks).
+
+The injected-variate parity of these datasets is in test_gpu_parity.py (fixtures
+ref_c3_* / ref_c4t_*, made by running the reference on them); here the configurations run
+as the benchmark runs them -- many chains from prior draws -- and are checked through
+properties that do not depend on the chain count:
+
+* config 3 (simulate_data.py pulsar, red.txt red noise, 5% outliers; 512 chains per GPU):
+  every chain finite and in the prior box, no status flags, the injected outliers found
+  (posterior outlier probability), the outlier fraction recovered, and the 512-chain
+  launch bitwise equal to two 256-chain launches keyed by global chain id;
+* config 4 (run_sims grid with the Student-t dof axis): one ragged batch of
+  {Gaussian, t_4} white noise x {outlier, no_outlier} x 5 models; the Student-t model's
+  dof posterior sits lower on the t_4 datasets than on the Gaussian ones.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a HIP device", allow_module_level=True)
+
+from gibbs_student_t_amd import data, run_sims  # noqa: E402
+from gibbs_student_t_amd.model import PTA  # noqa: E402
+from gibbs_student_t_amd.native import NativeSampler  # noqa: E402
+
+BETA = run_sims.MODELS["beta"]
+BETA_M = 0.01           # Gibbs(m=0.01) default prior mean of theta (gibbs.py:9)
+
+
+def _prior_init(pta, C, c0, seed=7):
+    n, m = pta.T.shape
+    lo = np.array([p.pmin for p in pta.params])
+    hi = np.array([p.pmax for p in pta.params])
+    x = np.stack([np.random.default_rng([seed, c0 + c]).uniform(lo, hi) for c in range(C)])
+    return dict(x=x, b=np.zeros((C, m)), z=np.ones((C, n)), alpha=np.ones((C, n)),
+                pout=np.zeros((C, n)), theta=np.full(C, 0.01), nu=np.full(C, 4.0))
+
+
+def test_config3_512_chains_properties():
+    psr, _ = data.simulate_data(seed=2017, theta=0.05, red_source="red.txt")
+    pta = PTA(psr)
+    C, burn, S = 512, 300, 200
+    init = _prior_init(pta, C, 0)
+    ns = NativeSampler(pta, BETA, 0)
+    ns.alloc(C)
+    ns.set_state(**init)
+    ns.sweep(burn, seed=33, sweep0=0)
+    rec = ns.alloc_records(S, keys=("x", "pout", "theta"))
+    ns.sweep(S, records=rec, seed=33, sweep0=burn)
+    out = ns.get_state()
+    x = rec["x"].cpu().numpy()
+    assert np.all(out["status"] == 0)
+    assert np.all(np.isfinite(x)) and np.all(np.isfinite(out["b"]))
+    lo = np.array([p.pmin for p in pta.params])
+    hi = np.array([p.pmax for p in pta.params])
+    assert np.all((x >= lo) & (x <= hi))
+    zt = psr.meta["z_true"].astype(bool)
+    assert zt.sum() >= 3
+    pbar = rec["pout"].cpu().numpy().mean(axis=(0, 1))
+    # injected sigma_out = 1 us outliers on ~0.1 us error bars: most are found (an outlier
+    # whose N(0, 1 us) draw happens to be small is indistinguishable, so not all)
+    assert pbar[zt].mean() > 0.6 and np.median(pbar[~zt]) < 0.05
+    # theta | z ~ Beta(sum z + n m, n - sum z + n (1 - m)) (gibbs.py:185-198), so its
+    # posterior mean is (E[sum z] + n m) / 2n with E[sum z] = sum of E[pout]
+    n = pta.n
+    th = rec["theta"].cpu().numpy()
+    want = (pbar.sum() + n * BETA_M) / (2 * n)
+    assert abs(th.mean() - want) < 0.05 * want, (th.mean(), want)
+    # the 512-chain launch == two 256-chain launches (Philox keyed by global chain id)
+    halves = []
+    for h in range(2):
+        nh = NativeSampler(pta, BETA, 0)
+        nh.alloc(C // 2)
+        nh.set_state(**{k: v[h * C // 2:(h + 1) * C // 2] for k, v in init.items()})
+        nh.sweep(burn, seed=33, sweep0=0, chain0=h * C // 2)
+        nh.sweep(S, seed=33, sweep0=burn, chain0=h * C // 2)
+        halves.append(nh.get_state())
+        nh.close()
+    for k in ("x", "b", "z", "alpha", "pout", "theta", "nu"):
+        np.testing.assert_array_equal(out[k], np.concatenate([hh[k] for hh in halves]), k)
+    ns.close()
+
+
+def test_config4_dof_grid_batch():
+    grid = run_sims.build_grid(thetas=(0.05,), realisations=1, dofs=(None, 4.0))
+    assert len(grid) == 20 and {e.dof for e in grid} == {None, 4.0}
+    per, burn, S = 16, 300, 200
+    st = run_sims.Study(grid, chains=per, seed=2017)
+    recs, _ = st.run(burn + S, burn=burn, keys=("x", "nu", "theta"))
+    out = st.ns.get_state()
+    st.close()
+    assert np.all(out["status"] == 0)
+    assert np.all(np.isfinite(recs["x"]))
+    nu_t = {}
+    for i, e in enumerate(grid):
+        nu = recs["nu"][i]
+        assert np.all((nu >= 1) & (nu <= 30))
+        if e.model == "t" and e.kind == "no_outlier":
+            nu_t[e.dof] = nu.mean()
+    # Student-t(4) white noise pulls the dof posterior down; Gaussian noise lets it rise
+    assert nu_t[4.0] < nu_t[None], nu_t

@@ -84,13 +84,14 @@ def test_stage_methods_and_reproducibility():
     for seed in (11, 11, 12):
         g = Gibbs(ref["pta"], **ref["kw"], seed=seed)
         x = ref["xs"]
+        # one sweep written out as the reference's loop body (gibbs.py:367-380)
         x = g.update_white_params(x)
         x = g.update_hyper_params(x)
-        b = g.update_b(x)
-        th = g.update_theta(x)
-        z = g.update_z(x)
-        a = g.update_alpha(x)
-        nu = g.update_df(x)
+        g._b = b = g.update_b(x)
+        g._theta = th = g.update_theta(x)
+        g._z = z = g.update_z(x)
+        g._alpha = a = g.update_alpha(x)
+        g.tdf = nu = g.update_df(x)
         assert b.shape == (ref["pta"].T.shape[1],) and z.shape == a.shape == (ref["pta"].n,)
         assert 0.0 <= th <= 1.0 and 1 <= nu <= 30
         runs.append((x.copy(), b.copy(), z.copy(), a.copy()))
@@ -98,6 +99,50 @@ def test_stage_methods_and_reproducibility():
     for u, v in zip(runs[0], runs[1]):
         np.testing.assert_array_equal(u, v)                   # same seed: same chain
     assert not np.array_equal(runs[0][1], runs[2][1])         # other seed: other draw
+
+
+def test_stage_methods_return_without_committing():
+    """gibbs.py:145-259: update_b/theta/z/alpha/df RETURN draws; the latent state changes
+    only when the caller assigns it (gibbs.py:374-380); update_z records _pout (:225)."""
+    ref = load_ref("beta_fixed")
+    g = Gibbs(ref["pta"], **ref["kw"], seed=5)
+    s = sweep_state(ref, 3)
+    _load_state(g, s)
+    x = ref["chain"][3]
+    before = {k: np.array(getattr(g, k), copy=True) for k in ("_b", "_z", "_alpha", "_theta",
+                                                               "tdf", "_pout")}
+    b1, b2 = g.update_b(x), g.update_b(x)
+    th1, th2 = g.update_theta(x), g.update_theta(x)
+    a1 = g.update_alpha(x)
+    nu1 = g.update_df(x)
+    for k in ("_b", "_z", "_alpha", "_theta", "tdf", "_pout"):
+        np.testing.assert_array_equal(getattr(g, k), before[k], err_msg=k)
+    assert not np.array_equal(b1, b2) and th1 != th2          # fresh draws per call
+    assert a1.shape == s["alpha"].shape and 1 <= nu1 <= 30
+    orc = Oracle(ref["pta"], OutlierModel(**ref["kw"]))
+
+    def pout_oracle():
+        st = ChainState(b=np.array(g._b), z=np.array(g._z), alpha=np.array(g._alpha),
+                        pout=np.array(g._pout), theta=float(g._theta), nu=float(g.tdf))
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            return orc.outlier_prob(st, x)
+
+    z1 = g.update_z(x)
+    np.testing.assert_array_equal(g._z, before["_z"])          # z not committed ...
+    np.testing.assert_allclose(g._pout, pout_oracle(), rtol=1e-10, atol=0)   # ... _pout is
+    assert set(np.unique(z1)) <= {0.0, 1.0}
+    # the reference's sweep commits by assignment; later stages then see the new values
+    g._b = b1
+    g._theta = th1
+    np.testing.assert_array_equal(g._b, b1)
+    g.update_z(x)
+    np.testing.assert_allclose(g._pout, pout_oracle(), rtol=1e-10, atol=0)
+    # get_lnlikelihood_df (gibbs.py:331-335) per chain
+    assert np.isclose(g.get_lnlikelihood_df(4), orc.df_logdensity(
+        ChainState(b=g._b, z=g._z, alpha=g._alpha, pout=g._pout, theta=g._theta, nu=4), 4),
+        rtol=1e-12)
+    g.close()
 
 
 def test_batched_chains_and_thinning():

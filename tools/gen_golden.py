@@ -316,6 +316,31 @@ def scaled(niter=6):
               np.nanmax(out["tape_b_cond"]), file=sys.stderr)
 
 
+def configs34(niter=12):
+    """Datasets of BASELINE configs 3 and 4 run through the reference.
+
+    * ``c3``: the config-3 pulsar -- simulate_data.py restatement with 5% outliers and the
+      reference's red.txt red-noise realisation (bench.py --config 3 uses seed 2017).
+    * ``c4t``: a config-4 Student-t white-noise dataset -- the run_sims grid's first
+      (theta = 0.05, dof = 4) realisation, seeded exactly as run_sims.build_grid seeds it.
+    """
+    c3, _ = gdata.simulate_data(seed=2017, theta=0.05, red_source="red.txt")
+    sd = int(np.random.SeedSequence([2017, 0, 0, 1]).generate_state(1)[0])
+    c4, _ = gdata.simulate_data(sd, theta=0.05, dof=4.0)
+    for tag, psr, models in (("c3", c3, ("beta", "t", "uniform")),
+                             ("c4t", c4, ("beta", "t", "gaussian"))):
+        pta_c = PTA(psr)
+        np.savez_compressed(os.path.join(OUTDIR, f"{tag}_dataset.npz"),
+                            **dataset_arrays(pta_c, psr))
+        for j, name in enumerate(models):
+            out = run_one(pta_c, name, MODELS[name], seed=5100 + 31 * j + len(tag),
+                          niter=niter, x0=[4.33, -14.0, -7.6])
+            out["model_kw"] = np.array(repr(MODELS[name]))
+            np.savez_compressed(os.path.join(OUTDIR, f"ref_{tag}_{name}_fixed.npz"), **out)
+            print(tag, name, "n", pta_c.n, "cond:", np.nanmax(out["tape_b_cond"]),
+                  file=sys.stderr)
+
+
 def main():
     os.makedirs(OUTDIR, exist_ok=True)
     niter = 12
@@ -324,6 +349,9 @@ def main():
         return
     if "--only-scaled" in sys.argv:
         scaled()
+        return
+    if "--only-configs34" in sys.argv:
+        configs34(niter)
         return
     psr = gdata.j1713(seed=1713, theta=0.05)
     pta = PTA(psr)
@@ -367,6 +395,7 @@ def main():
     np.savez_compressed(os.path.join(OUTDIR, "ref_twob_uniform_fixed.npz"), **out)
     simclean(niter)
     scaled()
+    configs34(niter)
 
 
 if __name__ == "__main__":
