@@ -3,8 +3,8 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--chains C] [--config 2|3|4|5]
 
 A *step* is one Gibbs sweep (gibbs.py:354-380) of every chain on every rank.  Each rank owns
-C chains (weak scaling; default 2048 per GPU = two chains per SIMD, the "1024+" of the
-BASELINE metric) of the run_sims.py 'beta' outlier-mixture model (run_sims.py:98-99) on
+C chains (weak scaling; default 2048 per GPU = two chains per SIMD, the "1024+ batched
+chains" of the BASELINE metric) of the run_sims.py 'beta' outlier-mixture model (run_sims.py:98-99) on
 J1713+0747's 130 TOAs.  The timed region is exactly K sweeps in one persistent launch,
 recording every sweep's full state (chain, bchain, zchain, alphachain, poutchain,
 thetachain, dfchain) to HBM as the reference records every sweep.
@@ -17,8 +17,8 @@ sampling; the collectives are the final all-gather of every chain's post-burn-in
 (global split-R-hat and bulk-ESS over ALL chains) and a max-reduce of the timings.
 
 ESS/s has its own window, independent of --steps: after the timed region every chain
-runs ``--ess-burn`` more sweeps (discarded), then ``--ess-window`` recorded sweeps of the
-sampled parameters and theta, timed on their own; ESS/s = min over quantities of the
+runs ``--ess-burn`` more sweeps (discarded), then ``--ess-window`` sweeps whose sampled
+parameters and theta are recorded every ``--ess-thin``-th sweep, timed on their own; ESS/s = min over quantities of the
 bulk-ESS summed over datasets / window seconds, reported only when every global R-hat is
 <= 1.01 (else null, with the reason).
 """
@@ -106,7 +106,8 @@ def config_datasets(config: int):
 def workload(config: int, rank: int, world: int, chains: int | None):
     """This rank's share of a BASELINE.json config.
 
-    2: J1713+0747 epochs, 2048 chains per GPU (weak scaling; the headline, default);
+    2: J1713+0747 epochs, 2048 chains per GPU (weak scaling; the headline, default: two
+       chains per SIMD, the "1024+" of the BASELINE metric; --chains 1024 for one per SIMD);
     3: simulate_data.py pulsar, 5% outliers, red.txt red noise, 512 chains per GPU
        (4096 over 8 GPUs; weak scaling);
     4: run_sims.py grid: 256 datasets (3 outlier fractions x {Gaussian, Student-t nu=4}
@@ -273,17 +274,18 @@ class StubSampler:
         return {k: torch.zeros((self.C, nrec) + shapes.get(k, (1,)), dtype=torch.float64)
                 for k in keys}
 
-    def sweep(self, nsweeps, records=None, seed=0, sweep0=0, chain0=0, **_):
+    def sweep(self, nsweeps, records=None, record_every=1, seed=0, sweep0=0, chain0=0, **_):
         import torch
         r = self.RHO
         for it in range(nsweeps):
             for c in range(self.C):
                 rng = np.random.default_rng([seed, chain0 + c, sweep0 + it])
-                if records is not None:
+                if records is not None and it % record_every == 0:
+                    ri = it // record_every
                     if "x" in records:
-                        records["x"][c, it] = torch.from_numpy(self.x[c])
+                        records["x"][c, ri] = torch.from_numpy(self.x[c])
                     if "theta" in records:
-                        records["theta"][c, it] = float(self.theta[c])
+                        records["theta"][c, ri] = float(self.theta[c])
                 e = rng.standard_normal(self.P + 1)
                 self.x[c] = r * self.x[c] + np.sqrt(1 - r * r) * e[:self.P]
                 self.theta[c] = r * self.theta[c] + np.sqrt(1 - r * r) * e[self.P]
@@ -322,9 +324,8 @@ def global_diagnostics(draws: np.ndarray, theta: np.ndarray, dsid: np.ndarray,
         if theta_on[d]:
             series["theta"] = theta[sel]
         for k, v in series.items():
-            e = diag.bulk_ess(v)
+            e, r = diag.ess_rhat(v)
             ess[k] += e if np.isfinite(e) else 0.0
-            r = diag.split_rhat(v)
             rhat[k] = max(rhat[k], r if np.isfinite(r) else np.inf)
     return ess, rhat
 
@@ -343,7 +344,9 @@ def main():
                     help="extra discarded sweeps before the ESS window (default 3000; "
                          "config 5: no ESS window)")
     ap.add_argument("--ess-window", type=int, default=None,
-                    help="recorded sweeps of the ESS window (default 1000; config 5: 0)")
+                    help="sweeps of the ESS window (default 5000; config 5: 0)")
+    ap.add_argument("--ess-thin", type=int, default=5,
+                    help="record every k-th sweep of the ESS window (default 5)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
@@ -364,7 +367,9 @@ def main():
         secs = args.cpu_seconds if args.config != 5 else max(args.cpu_seconds, 20.0)
         cpu = cpu_baseline(args.config, secs, cores)      # before the GPU is touched
     ess_burn = args.ess_burn if args.ess_burn is not None else (0 if args.config == 5 else 3000)
-    ess_win = args.ess_window if args.ess_window is not None else (0 if args.config == 5 else 1000)
+    ess_win = args.ess_window if args.ess_window is not None else (0 if args.config == 5 else 5000)
+    thin = max(1, args.ess_thin)
+    ess_win = (ess_win // thin) * thin
 
     import torch
     rank, local, world = dist.init("gloo" if args.stub else None)
@@ -421,8 +426,8 @@ def main():
     if ess_win > 0:
         if ess_burn > 0:
             ns.sweep(ess_burn, seed=args.seed, sweep0=W + K, chain0=c0)
-        wrec = ns.alloc_records(ess_win, keys=("x", "theta"))
-        win_s = timed(lambda: ns.sweep(ess_win, records=wrec, seed=args.seed,
+        wrec = ns.alloc_records(ess_win // thin, keys=("x", "theta"))
+        win_s = timed(lambda: ns.sweep(ess_win, records=wrec, record_every=thin, seed=args.seed,
                                        sweep0=W + K + ess_burn, chain0=c0))
         draws = dist.gather_chains(torch.cat([wrec["x"], wrec["theta"][..., None]], dim=2)
                                    .cpu().numpy(), dev)
@@ -513,7 +518,7 @@ def main():
                                       "RCCL only for the final all-gather of chain draws"},
             "ess_per_sec": ess_ps,
             "ess_per_sec_reason": reason,
-            "ess_window": {"burn_in_sweeps": W + K + ess_burn, "sweeps": ess_win,
+            "ess_window": {"burn_in_sweeps": W + K + ess_burn, "sweeps": ess_win, "thin": thin,
                            "seconds": win_s, "chains": C * world,
                            "ess_total": ess, "rhat_max": rhat},
             "shards": [[int(a), int(b)] for a, b in shards],   # global chain ids per rank

@@ -40,6 +40,8 @@ struct Ctx {
   int nd = 0, nmax = 0, m = 0, raug = 0;
   int MT = 0, NS = 0, K0 = 0, WPB = 4;
   int ncu = 256;                   // compute units of the device (workgroup sizing)
+  double* tmfac = nullptr;         // persistent path: timing-model factor scratch
+  size_t tmfac_bytes = 0;
   int path_req = GST_PATH_AUTO;    // gst_set_path
   int path = GST_PATH_PERSISTENT;  // chosen by gst_model_set
   std::vector<void*> allocs;
@@ -71,6 +73,12 @@ int upload(Ctx* cx, const void* host, size_t bytes, void** dev) {
   return 0;
 }
 
+void free_tmfac(Ctx* cx) {
+  if (cx->tmfac) (void)hipFree(cx->tmfac);
+  cx->tmfac = nullptr;
+  cx->tmfac_bytes = 0;
+}
+
 void free_model(Ctx* cx) {
   for (void* p : cx->allocs) (void)hipFree(p);
   cx->allocs.clear();
@@ -79,27 +87,31 @@ void free_model(Ctx* cx) {
   cx->nd = 0;
   cx->has_model = false;
   free_scratch(cx);
+  free_tmfac(cx);
 }
 
 typedef void (*kfn_t)(const gst::DevModel*, const gst::DevState, const gst::DevRec,
                       const gst::DevTape, int, int, long long, int, unsigned,
                       unsigned long long, long long, int, double*, double*);
 
-template <int MT, int NS, int K0, int RA, bool TAPE, int WPB = gst::wpb_for(MT, NS)>
+template <int MT, int NS, int K0, int RA, bool TAPE, int WPB = 4, int OCC = 1>
 kfn_t kfn() {
-  return &gst::gst_sweep_kernel<MT, NS, K0, RA, TAPE, WPB>;
+  return &gst::gst_sweep_kernel<MT, NS, K0, RA, TAPE, WPB, OCC>;
 }
 
 // Instantiated shapes: MT = padded matrix dim / 8, NS = TOA slots of 64, K0 = timing-model
 // panels of 8, RA = augmented-row index = 8*K0 + nfourier (the elimination length).
-// wpb: chains per workgroup (the default, wpb_for, or 2 / 1 for sampling launches with
-// fewer chains than fill every SIMD; tape-mode parity launches always use the default).
-kfn_t pick(int MT, int NS, int K0, int RA, bool tape, int wpb) {
+// wpb: chains per workgroup (4, or 2 / 1 for sampling launches with fewer chains than
+// fill every SIMD; tape-mode parity launches always use 4).  occ2: the two-chains-per-SIMD
+// build (256 registers per lane), picked when the launch has more chains than SIMDs; with
+// at most one chain per SIMD the uncapped build keeps more of each chain in registers.
+kfn_t pick(int MT, int NS, int K0, int RA, bool tape, int wpb, bool occ2) {
 #define GST_CASE(mt, ns, k0, ra)                                                  \
   if (MT == mt && NS == ns && K0 == k0 && RA == ra) {                             \
     if (tape) return kfn<mt, ns, k0, ra, true>();                                 \
     if (wpb == 1) return kfn<mt, ns, k0, ra, false, 1>();                         \
     if (wpb == 2) return kfn<mt, ns, k0, ra, false, 2>();                         \
+    if (occ2 && gst::occ_for(mt, k0) == 2) return kfn<mt, ns, k0, ra, false, 4, 2>(); \
     return kfn<mt, ns, k0, ra, false>();                                          \
   }
   GST_CASE(10, 2, 2, 76)   // J1713-like, n <= 128 (no_outlier datasets)
@@ -368,7 +380,7 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
   const int MT = mpad / 8, K0 = ntm_pad / 8;
   const int nsl = (nmax + 63) / 64;
   const int NS = nsl <= 2 ? 2 : (nsl <= 3 ? 3 : 4);
-  const bool fits = round_up(nmax, 4) <= 64 * NS && pick(MT, NS, K0, raug, false, 4);
+  const bool fits = round_up(nmax, 4) <= 64 * NS && pick(MT, NS, K0, raug, false, 4, false);
   int path = cx->path_req;
   if (path == GST_PATH_AUTO) path = fits ? GST_PATH_PERSISTENT : GST_PATH_LARGE;
   if (path == GST_PATH_PERSISTENT && !fits) {
@@ -404,7 +416,7 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
   cx->K0 = K0;
   cx->raug = raug;
   cx->m = m;
-  cx->WPB = gst::wpb_for(MT, NS);
+  cx->WPB = 4;
   cx->path = path;
   if (path == GST_PATH_LARGE) {
     const gst::DevModel& h = hmd[0];
@@ -539,8 +551,8 @@ static int launch(Ctx* cx, const gst_state* s, const gst_records* r, const gst_t
   const bool tape = tp && tp->data;
   if (!s->dataset && cx->nd > 1)
     return fail("gst: the model has several datasets: state.dataset must be set");
-  gst::DevState ds{s->x,     s->b,  s->z,      s->alpha,  s->pout,
-                   s->theta, s->nu, s->status, s->dataset, cx->nmax, cx->nd};
+  gst::DevState ds{s->x,     s->b,  s->z,      s->alpha,   s->pout, s->theta,
+                   s->nu,    s->status, s->dataset, cx->nmax, cx->nd, nullptr};
   gst::DevRec dr{};
   if (r) dr = gst::DevRec{r->x, r->b, r->z, r->alpha, r->pout, r->theta, r->nu, r->nrec};
   else record_every = 0;
@@ -556,8 +568,17 @@ static int launch(Ctx* cx, const gst_state* s, const gst_records* r, const gst_t
     if (wpb >= 1 && C <= cx->ncu) wpb = 1;
     else if (wpb >= 2 && C <= 2 * cx->ncu) wpb = 2;
   }
-  kfn_t k = pick(cx->MT, cx->NS, cx->K0, cx->raug, tape, wpb);
+  kfn_t k = pick(cx->MT, cx->NS, cx->K0, cx->raug, tape, wpb, C > 4 * cx->ncu);
   if (!k) return fail("gst: no kernel instance");
+  // timing-model factor scratch: [C][slots with s < K0][64] doubles
+  const int ntms = cx->MT * (cx->MT + 1) / 2 - (cx->MT - cx->K0) * (cx->MT - cx->K0 + 1) / 2;
+  const size_t need = (size_t)C * ntms * 64 * sizeof(double);
+  if (need > cx->tmfac_bytes) {
+    free_tmfac(cx);
+    HIP_OK(hipMalloc(&cx->tmfac, need));
+    cx->tmfac_bytes = need;
+  }
+  ds.tmfac = cx->tmfac;
   const dim3 grid((C + wpb - 1) / wpb), block(64 * wpb);
   hipStream_t st = (hipStream_t)stream;
   HIP_OK(hipEventRecord(cx->ev0, st));

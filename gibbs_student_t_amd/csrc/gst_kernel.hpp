@@ -31,22 +31,37 @@ namespace gst {
 
 typedef double v4d __attribute__((ext_vector_type(4)));
 
-__host__ __device__ constexpr int CQ(int MT) { return 8 * MT + ((4 - 8 * MT) % 32 + 32) % 32; }
-
-// waves (chains) per workgroup: as many as the per-wave LDS footprint allows (one
-// workgroup per CU at these sizes; never more than 4 = one wave per SIMD)
-__host__ __device__ constexpr int wpb_for(int MT, int NS) {
-#ifdef GST_WPB_OVERRIDE  // diagnostic builds only (per-CU contention experiments)
-  return GST_WPB_OVERRIDE;
-#endif
-  return (8 * CQ(MT) + 16 * 17 + 64 * NS + 9 * 8 * MT + 32 + 128 +
-          64 * ((MT - 2) * (MT - 1) / 2)) * 8 * 4 <= 160 * 1024
-             ? 4
-             : 2;
-}
 constexpr int NWHITE = 20;
 constexpr int NHYPER = 10;
+__host__ __device__ constexpr int SL(int r, int s) { return r * (r + 1) / 2 + s; }
 
+// Per-chain LDS (doubles), laid out so that two chains fit per SIMD (8 per CU, 20 KB each
+// at J1713 sizes):
+//   S0R   [64 * SL(MT-K0, 0)]  the Schur complement S0 during the hyper block, [slot][lane];
+//                              outside it, scratch of the other stages (white MH variates,
+//                              Gram weights + tile transposes, b-draw vectors, nu grid)
+//   colq  [8 * MT]             the one published column of the elimination, [p][r]
+//   mhh   [4 * NHYPER]         hyper-MH variates of the sweep
+//   phbuf [8 * MT]             phi^-1 by internal column
+// index of slot (r, s), s < K0, among the timing-model factor slots (column-major)
+__host__ __device__ constexpr int tm_slot(int MT, int r, int s) {
+  return s * MT - s * (s - 1) / 2 + (r - s);
+}
+__host__ __device__ constexpr int s0r_doubles(int MT, int K0) { return 64 * SL(MT - K0, 0); }
+__host__ __device__ constexpr int lds_doubles(int MT, int K0) {
+  return s0r_doubles(MT, K0) + 8 * MT + 4 * NHYPER + 8 * MT;
+}
+// chains (waves) per SIMD the LDS allows with 4-chain workgroups: 2 when two workgroups
+// (8 chains) fit a CU's 160 KB
+__host__ __device__ constexpr int occ_for(int MT, int K0) {
+  return lds_doubles(MT, K0) * 8 * 4 * 2 <= 160 * 1024 ? 2 : 1;
+}
+// scratch aliases inside S0R (offsets in doubles), each live only while S0 is dead
+__host__ __device__ constexpr int s0r_need(int MT, int NS) {
+  return (4 * NWHITE > 64 * NS + 16 * 17 ? 4 * NWHITE : 64 * NS + 16 * 17) > 7 * 8 * MT + 64
+             ? (4 * NWHITE > 64 * NS + 16 * 17 ? 4 * NWHITE : 64 * NS + 16 * 17)
+             : 7 * 8 * MT + 64;
+}
 struct DevModel {
   const double* Tmf;     // [nks][NT][64]: MFMA-packed augmented T, internal column order
   const double* Tcol;    // [m][npad]: T column-major, reference column order, zero padded
@@ -83,6 +98,7 @@ struct DevState {
   const int* dataset;  // [C] dataset of each chain (null: every chain uses dataset 0)
   int nst;             // row stride of the per-TOA arrays (max n over the datasets)
   int nd;              // number of datasets
+  double* tmfac;       // [C][timing-model factor slots][64] scratch (persistent path)
 };
 struct DevRec {
   double *x, *b, *z, *alpha, *pout, *theta, *nu;
@@ -96,16 +112,10 @@ struct DevTape {
 // tape layout offsets (see gst.h)
 constexpr int TP_WHITE = 0, TP_HYPER = 80, TP_DELTA = 120;
 
-__host__ __device__ constexpr int SL(int r, int s) { return r * (r + 1) / 2 + s; }
-
-// Published-column buffers: colq[q][p][r] (row 8r+p of the column with residue q), r
-// fastest, so a lane's row-side (p) and column-side (q) reads are contiguous in r and go as
-// 128-bit LDS loads.  The publishing stores stay 64-bit: with ds_write_b128 here the
-// same-wave loads that follow returned stale data on MI355X (wrong factors, run-to-run
-// different; measured, round 1), with ds_write_b64 they are exact.  Per-q stride CQ = 8*MT rounded up to 4 mod 32 doubles: with the
-// row stride MT = 10, the 16 lanes (p in {0,1}, q in 0..7) of a publishing ds_write_b128
-// then cover 16 distinct 16-byte bank groups.
-// (CQ: see the published-column buffers below)
+// The published column: colq[p][r] = row 8r+p of the column being eliminated, r fastest, so
+// a lane's row-side (p) and column-side (q) reads are contiguous in r and go as 128-bit LDS
+// loads; the 8 owner lanes (q == column residue) write it.  Row stride MT = 10 doubles puts
+// the 8 p-rows of a 128-bit read in distinct bank groups (80 B apart).
 
 #ifdef GST_STAMPS
 #define GST_STAMP_DECL \
@@ -186,11 +196,15 @@ __device__ __forceinline__ double rsqrt_nr(double a) {
   return y;
 }
 
+// Hand-off point between lanes of one wave through LDS.  LDS instructions of a wave execute
+// in issue order, so no hardware wait is needed; what must not happen is the COMPILER moving
+// a load that reads another lane's data above the store that wrote it (from one lane's
+// point of view the two addresses differ, so a single-thread fence does not forbid it).  A
+// wavefront-scope fence is the construct that orders memory accesses across the lanes of
+// the wave; it emits no instruction.
 __device__ __forceinline__ void lds_order() {
-  // Same-wave LDS accesses execute in issue order; this only stops the compiler from
-  // moving memory operations across the hand-off point.
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
 __device__ __forceinline__ double pget(const double (&x)[4], int i) {
@@ -215,36 +229,95 @@ __device__ __forceinline__ int bern_legacy(double p, double u) {
   return u > exp(log(1.0 - qq)) ? 0 : 1;
 }
 
-// Box-Muller normal from one Philox draw.
+// cos(2 pi u) for u in [0, 1): folded to a quarter turn, then the Taylor series of cos or
+// sin on [0, pi/4] (truncation < 1e-16), chosen by select.  Lighter than OCML's cospi
+// (fewer live registers inside the per-TOA gamma loops).
+__device__ __forceinline__ double cos2pi(double u) {
+  double x = u < 0.5 ? u : 1.0 - u;            // cos(2 pi (1 - u)) = cos(2 pi u)
+  const double sg = x > 0.25 ? -1.0 : 1.0;     // cos(2 pi (1/2 - x)) = -cos(2 pi x)
+  x = x > 0.25 ? 0.5 - x : x;                  // x in [0, 1/4]
+  const bool sn = x > 0.125;                   // cos(2 pi x) = sin(2 pi (1/4 - x))
+  const double t = (sn ? 0.25 - x : x) * 6.283185307179586477;   // t in [0, pi/4]
+  const double t2 = t * t;
+  double c = 1.0 / 20922789888000.0;           // 1/16!
+  c = fma(c, t2, -1.0 / 87178291200.0);
+  c = fma(c, t2, 1.0 / 479001600.0);
+  c = fma(c, t2, -1.0 / 3628800.0);
+  c = fma(c, t2, 1.0 / 40320.0);
+  c = fma(c, t2, -1.0 / 720.0);
+  c = fma(c, t2, 1.0 / 24.0);
+  c = fma(c, t2, -0.5);
+  c = fma(c, t2, 1.0);
+  double sv = 1.0 / 355687428096000.0;         // 1/17!
+  sv = fma(sv, t2, -1.0 / 1307674368000.0);
+  sv = fma(sv, t2, 1.0 / 6227020800.0);
+  sv = fma(sv, t2, -1.0 / 39916800.0);
+  sv = fma(sv, t2, 1.0 / 362880.0);
+  sv = fma(sv, t2, -1.0 / 5040.0);
+  sv = fma(sv, t2, 1.0 / 120.0);
+  sv = fma(sv, t2, -1.0 / 6.0);
+  sv = fma(sv, t2, 1.0) * t;
+  return sg * (sn ? sv : c);
+}
+
+// sin(2 pi u) = cos(2 pi (u - 1/4)), the argument wrapped back into [0, 1)
+__device__ __forceinline__ double sin2pi(double u) {
+  return cos2pi(u < 0.25 ? u + 0.75 : u - 0.25);
+}
+
+// Box-Muller normal from one Philox draw (its cosine half).
 __device__ __forceinline__ double normal_from(const Rng& rng, uint32_t index, uint32_t tag) {
   double a, b;
   rng.uniform2(index, tag, a, b);
-  return sqrt(-2.0 * log(1.0 - a)) * cospi(2.0 * b);
+  return sqrt(-2.0 * log(1.0 - a)) * cos2pi(b);
 }
 
-// Marsaglia-Tsang Gamma(a, 1); a < 1 via the a+1 boost.  Bounded attempts.
+// Both Box-Muller normals of one Philox draw: normals 2k and 2k + 1 of a stream.
+__device__ __forceinline__ void normal_pair(const Rng& rng, uint32_t k, uint32_t tag,
+                                            double& n0, double& n1) {
+  double a, b;
+  rng.uniform2(k, tag, a, b);
+  const double r = sqrt(-2.0 * log(1.0 - a));
+  n0 = r * cos2pi(b);
+  n1 = r * sin2pi(b);
+}
+
+// Normal j of a stream (one element of normal_pair(j / 2)).
+__device__ __forceinline__ double normal_k(const Rng& rng, uint32_t j, uint32_t tag) {
+  double n0, n1;
+  normal_pair(rng, j >> 1, tag, n0, n1);
+  return (j & 1u) ? n1 : n0;
+}
+
+// Marsaglia-Tsang Gamma(a, 1); a < 1 via the a+1 boost.  Attempts go in pairs: one Philox
+// draw gives both Box-Muller normals, a second the two acceptance uniforms.  Bounded.
 __device__ double gamma_mt(double a, const Rng& rng, uint32_t index, uint32_t tag) {
   double boost = 1.0;
   if (a < 1.0) {
     double ub, unused;
     rng.uniform2(index, tag | 0xFFFFFFu, ub, unused);
-    boost = pow(1.0 - ub, 1.0 / a);
+    boost = exp(log(1.0 - ub) / a);
     a += 1.0;
   }
   const double d = a - 1.0 / 3.0;
   const double cc = 1.0 / sqrt(9.0 * d);
 #pragma unroll 1
-  for (uint32_t att = 0; att < 256u; ++att) {
-    double u1, u2, u3, u4;
+  for (uint32_t att = 0; att < 128u; ++att) {
+    double u1, u2, ua, ub;
     rng.uniform2(index, tag | (2u * att), u1, u2);
-    rng.uniform2(index, tag | (2u * att + 1u), u3, u4);
-    const double xn = sqrt(-2.0 * log(1.0 - u1)) * cospi(2.0 * u2);
-    double v = 1.0 + cc * xn;
-    if (v <= 0.0) continue;
-    v = v * v * v;
-    const double x2 = xn * xn;
-    if (u3 < 1.0 - 0.0331 * x2 * x2) return d * v * boost;
-    if (log(u3) < 0.5 * x2 + d * (1.0 - v + log(v))) return d * v * boost;
+    rng.uniform2(index, tag | (2u * att + 1u), ua, ub);
+    const double r = sqrt(-2.0 * log(1.0 - u1));
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const double xn = r * (h == 0 ? cos2pi(u2) : sin2pi(u2));
+      const double u3 = h == 0 ? ua : ub;
+      double v = 1.0 + cc * xn;
+      if (v <= 0.0) continue;
+      v = v * v * v;
+      const double x2 = xn * xn;
+      if (u3 < 1.0 - 0.0331 * x2 * x2) return d * v * boost;
+      if (log(u3) < 0.5 * x2 + d * (1.0 - v + log(v))) return d * v * boost;
+    }
   }
   return d * boost;
 }
@@ -266,7 +339,8 @@ __device__ double gamma_mt(double a, const Rng& rng, uint32_t index, uint32_t ta
 // these columns, as mantissa product + exponent sum), sum a_{raug,k}^2 / a_kk (= the
 // d^T Sigma^-1 d contribution) and the failure flag.
 struct CholCtx {
-  double* colq;   // [8][MP]
+  double* colq;   // [8][MT] the published column
+  double* junk;   // [8][MT] where the other lanes' publishing stores land (see chol_publish)
   int lane, p, q, raug;
   double mant, quad;
   int expo, fail;
@@ -275,9 +349,13 @@ struct CholCtx {
   double apr[2], zr[2];
 };
 
-template <int MT>
+// Publish column 8s + QQ: its owner lanes (q == QQ) write their slot column s, rows >= s.
+// Every lane stores ("pad, don't mask"): the others' stores go to the junk rows, so the
+// elimination stays free of lane-divergent control flow, which at this register pressure
+// makes the allocator spill kilobytes per lane.
+template <int MT, int QQ>
 __device__ __forceinline__ void chol_publish(const double (&L)[SL(MT, 0)], CholCtx& cc, int s) {
-  double* dst = cc.colq + CQ(MT) * cc.q + MT * cc.p;
+  double* dst = (cc.q == QQ ? cc.colq : cc.junk) + MT * cc.p;
 #pragma unroll
   for (int r2 = 0; r2 < MT; r2 += 2) {          // rows (r2, r2+1)
     if (r2 >= s) {
@@ -312,15 +390,14 @@ __device__ __forceinline__ void pivot_rcp(ColView<MT>& c) {
   c.e = fma(-c.akk, c.y0, 1.0);
 }
 
-template <int MT, int K, int KK>
+template <int MT, int K>
 __device__ __forceinline__ void chol_load(const CholCtx& cc, ColView<MT>& c) {
-  static_assert(MT % 2 == 0 && CQ(MT) % 2 == 0, "128-bit column loads need 16-byte alignment");
-  const double* col = cc.colq + CQ(MT) * KK;
-  const double* cr = col + MT * cc.p;
-  const double* cq = col + MT * cc.q;
+  static_assert(MT % 2 == 0, "128-bit column loads need 16-byte alignment");
+  const double* cr = cc.colq + MT * cc.p;
+  const double* cq = cc.colq + MT * cc.q;
 #pragma unroll
   for (int r2 = 0; r2 < MT; r2 += 2) {          // rows (r2, r2+1)
-    if (r2 >= K) {  // 128-bit loads (16-byte aligned: CQ, MT, r2 even)
+    if (r2 >= K) {  // 128-bit loads (16-byte aligned: MT, r2 even)
       typedef double v2_t __attribute__((ext_vector_type(2)));
       const v2_t a = *(const v2_t*)(cr + r2);
       const v2_t b = *(const v2_t*)(cq + r2);
@@ -365,14 +442,15 @@ __device__ __forceinline__ void chol_step(double (&L)[SL(MT, 0)], CholCtx& cc,
     for (int r = K1; r < MT; ++r) L[SL(r, K1)] = fma(-cur.lr[r], tk, L[SL(r, K1)]);
 #endif
     if constexpr (NEXT) {
-      chol_publish<MT>(L, cc, K1);
+      lds_order();                   // column k's loads precede its overwrite
+      chol_publish<MT, KK1>(L, cc, K1);
 #ifdef GST_EXP_NOPIV  // timing experiment only: pivot chain cut
       nxt.akk = 2.0;
 #else
       nxt.akk = rdlane(L[SL(K1, K1)], 9 * KK1);
 #endif
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      chol_load<MT, K1, KK1>(cc, nxt);
+      lds_order();
+      chol_load<MT, K1>(cc, nxt);
       pivot_rcp<MT>(nxt);
     }
   }
@@ -397,13 +475,47 @@ __device__ __forceinline__ void chol_step(double (&L)[SL(MT, 0)], CholCtx& cc,
 template <int MT, int KLO, int KEND>
 __device__ __forceinline__ void chol_range(double (&L)[SL(MT, 0)], CholCtx& cc) {
   static_assert(KEND > 8 * KLO && KEND <= 8 * MT, "bad elimination range");
-  chol_publish<MT>(L, cc, KLO);
+  chol_publish<MT, 0>(L, cc, KLO);
   ColView<MT> c;
   c.akk = rdlane(L[SL(KLO, KLO)], 0);
   lds_order();
-  chol_load<MT, KLO, 0>(cc, c);
+  chol_load<MT, KLO>(cc, c);
   pivot_rcp<MT>(c);
   chol_step<MT, KLO, 0, KEND>(L, cc, c);
+  lds_order();
+}
+
+// The same elimination without the next column's prefetch (one ColView live instead of
+// two): used for the timing-model columns, where every slot of L is still live and the
+// register budget of two chains per SIMD has no room for the double buffer.
+template <int MT, int K, int KK, int KEND>
+__device__ __forceinline__ void chol_step_lean(double (&L)[SL(MT, 0)], CholCtx& cc) {
+  constexpr int k = 8 * K + KK;
+  constexpr int K1 = (KK == 7) ? K + 1 : K;
+  constexpr int KK1 = (KK + 1) & 7;
+  ColView<MT> cur;
+  lds_order();                       // the previous step's loads precede this publication
+  chol_publish<MT, KK>(L, cc, K);
+  cur.akk = rdlane(L[SL(K, K)], 9 * KK);
+  lds_order();
+  chol_load<MT, K>(cc, cur);
+  pivot_rcp<MT>(cur);
+  cur.lr[K] = (8 * K + cc.p > k) ? cur.lr[K] : 0.0;
+  cur.lc[K] = (8 * K + cc.q > k) ? cur.lc[K] : 0.0;
+  const double sk = fma(cur.y0, cur.e, cur.y0);
+#pragma unroll
+  for (int s = K; s < MT; ++s) {
+    if (KK == 7 && s == K) continue;   // slot column K is complete
+#pragma unroll
+    for (int r = s; r < MT; ++r) L[SL(r, s)] = fma(-(cur.lr[r] * sk), cur.lc[s], L[SL(r, s)]);
+  }
+  if constexpr (k + 1 < KEND) chol_step_lean<MT, K1, KK1, KEND>(L, cc);
+}
+
+template <int MT, int KLO, int KEND>
+__device__ __forceinline__ void chol_range_lean(double (&L)[SL(MT, 0)], CholCtx& cc) {
+  static_assert(KEND > 8 * KLO && KEND <= 8 * MT, "bad elimination range");
+  chol_step_lean<MT, KLO, 0, KEND>(L, cc);
   lds_order();
 }
 
@@ -466,11 +578,13 @@ __device__ __forceinline__ void chol_stats(CholCtx& cc) {
   cc.fail = __ballot(f) != 0ull ? 1 : 0;
 }
 
-// WPB = chains (waves) per workgroup: wpb_for(MT, NS) fills a CU with one chain per SIMD;
-// the host picks fewer when the launch has fewer chains than 4 x CUs, so the chains spread
-// over every CU instead of sharing the LDS of a quarter of them.
-template <int MT, int NS, int K0, int RA, bool TAPE, int WPB = wpb_for(MT, NS)>
-__global__ void __launch_bounds__(64 * WPB)
+// WPB = chains (waves) per workgroup (4 = one per SIMD; the host picks 2 or 1 when the
+// launch has fewer chains than CUs x 4, so the chains spread over every CU).  OCC = chains
+// per SIMD the kernel is compiled for: 2 caps it at 256 registers per lane (VGPR + AGPR)
+// so that two workgroups share a CU and each SIMD interleaves two chains' dependency
+// chains (the kernel is latency-bound per wave).
+template <int MT, int NS, int K0, int RA, bool TAPE, int WPB = 4, int OCC = 1>
+__global__ void __launch_bounds__(64 * WPB, OCC)
     gst_sweep_kernel(const DevModel* __restrict__ mds, const DevState st, const DevRec rec, const DevTape tape,
                      int C, int nsweeps, long long sweep0, int record_every, unsigned mask,
                      unsigned long long seed, long long chain0, int eval_only, double* out_w,
@@ -479,12 +593,11 @@ __global__ void __launch_bounds__(64 * WPB)
   constexpr int NT = MT / 2;          // 16-wide MFMA tiles
   constexpr int NTT = NT * (NT + 1) / 2;
   constexpr int MP = 8 * MT;
-  constexpr int NS0 = SL(MT - K0, 0);  // S0 slots (r >= s >= K0)
+  constexpr int NTMS = NSL - SL(MT - K0, 0);  // timing-model factor slots (s < K0)
   constexpr int TB_LD = 17;
-  static_assert(WPB >= 1 && WPB <= wpb_for(MT, NS), "workgroup exceeds the LDS budget");
-  constexpr int LDSW = 8 * CQ(MT) + 16 * TB_LD + 64 * NS + 9 * MP + 32 + 4 * 32;
-  __shared__ double smem[WPB][LDSW];
-  __shared__ double s0mem[WPB][NS0 * 64];   // Schur complement S0, [slot][lane]
+  constexpr int S0RD = s0r_doubles(MT, K0);
+  static_assert(s0r_need(MT, NS) <= S0RD, "S0 region too small for the stage scratch");
+  __shared__ double smem[WPB][lds_doubles(MT, K0)];
 
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -502,21 +615,32 @@ __global__ void __launch_bounds__(64 * WPB)
   const int p = lane >> 3, q = lane & 7;
   GST_STAMP_DECL
 
-  double* colq = smem[wv];            // [8][MP] published columns
-  double* tbuf = colq + 8 * CQ(MT);   // 16 x TB_LD Gram tile transpose
-  double* vbuf = tbuf + 16 * TB_LD;   // per-TOA scratch (weights), 64*NS
-  double* bbuf = vbuf + 64 * NS;      // b, reference order
-  double* phbuf = bbuf + MP;          // phi^-1 by internal index
-  double* zraw = phbuf + MP;          // a_{raug,k}
-  double* apiv = zraw + MP;           // pivots a_kk
-  double* wvec = apiv + MP;           // back-substitution rhs
-  double* xbuf = wvec + MP;           // scratch (Delta, solution; internal order)
-  double* yinv = xbuf + MP;           // 1/sqrt(a_kk)
-  double* dfbuf = yinv + MP;          // 32
-  double* mhv = dfbuf + 32;           // [30][4] MH variates: u_scale, index, jump, log(u_acc)
-  double* lfq = mhv + 4 * 32;         // log f_k of the power law (copy of md.lfreq)
-  double* ldq = lfq + MP;             // log df_k (copy of md.ldf)
-  double* S0 = s0mem[wv] + lane;      // S0[64 * slot]
+  double* S0R = smem[wv];             // S0 during the hyper block, else stage scratch
+  double* colq = S0R + S0RD;          // [8][MT] the published column
+  double* mhh = colq + 8 * MT;        // [10][4] hyper MH variates
+  double* phbuf = mhh + 4 * NHYPER;   // phi^-1 by internal index; eliminations' junk rows
+  double* S0 = S0R + lane;            // S0[64 * slot]
+  // scratch inside S0R (S0 is dead outside the hyper block):
+  double* mhw = S0R;                  // [20][4] white MH variates (sweep start .. white block)
+  double* vbuf = S0R;                 // Gram weights, 64*NS
+  double* tbuf = S0R + 64 * NS;       // 16 x TB_LD Gram tile transpose
+  double* zraw = S0R;                 // b draw: a_{raug,k}
+  double* apiv = zraw + MP;           //   pivots a_kk
+  double* wvec = apiv + MP;           //   back-substitution rhs
+  double* xbuf = wvec + MP;           //   Delta, solution (internal order)
+  double* yinv = xbuf + MP;           //   1/sqrt(a_kk)
+  double* bsc = yinv + MP;            //   b in reference order (T b input)
+  double* tdg = bsc + MP;             //   8 x 8 diagonal-block transposes
+  double* dfbuf = S0R;                // nu grid (32)
+  // the TM factor slots (s < K0) wait in global scratch while the hyper block runs
+  // per-chain rows of the state arrays: wave-uniform base pointers (SGPRs), so every
+  // per-lane access is base + 32-bit lane offset
+  double* const tmf = st.tmfac + (size_t)c * NTMS * 64;
+  double* const xrow = st.x + (size_t)c * md.P;
+  double* const brow = st.b + (size_t)c * md.m;
+  double* const zrow = st.z + (size_t)c * nst;
+  double* const arow = st.alpha + (size_t)c * nst;
+  double* const prow = st.pout + (size_t)c * nst;
 
   static_assert(RA >= 8 * K0 + 1 && RA < 8 * MT, "augmented row out of range");
   const int n = md.n, m = md.m, P = md.P;
@@ -534,18 +658,15 @@ __global__ void __launch_bounds__(64 * WPB)
   double xv[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int j = 0; j < 4; ++j)
-    if (j < P) xv[j] = st.x[(size_t)c * P + j];
+    if (j < P) xv[j] = xrow[j];
   double theta = st.theta[c];
   double nu = st.nu[c];
-  for (int j = lane; j < MP; j += 64) bbuf[j] = (j < m) ? st.b[(size_t)c * m + j] : 0.0;
+  for (int j = lane; j < MP; j += 64) bsc[j] = (j < m) ? brow[j] : 0.0;
   for (int j = lane; j < MP; j += 64) phbuf[j] = 0.0;
-  for (int j = lane; j < md.nf; j += 64) {
-    lfq[j] = md.lfreq[j];
-    ldq[j] = md.ldf[j];
-  }
 
-  double rr[NS], s2[NS], al[NS], po[NS], yv[NS];
-  int cls[NS];
+  // per-TOA chain state in registers: alpha, y = r - T b, pout and the z bits; the data
+  // (r, sigma^2, noise class) is re-read from the dataset's L2-resident arrays where used
+  double al[NS], yv[NS], po[NS];
   double wcls = 0.0;  // lane u < ncls: W_u of the current white block
   unsigned zb = 0u, vmask = 0u;
 #pragma unroll
@@ -553,15 +674,14 @@ __global__ void __launch_bounds__(64 * WPB)
     const int t = 64 * s + lane;
     const bool ok = t < n;
     vmask |= ok ? (1u << s) : 0u;
-    rr[s] = ok ? md.resid[t] : 0.0;
-    s2[s] = ok ? md.sig2[t] : 1.0;
-    cls[s] = (ok && md.cidx) ? md.cidx[t] : -1;
-    al[s] = ok ? st.alpha[(size_t)c * nst + t] : 1.0;
-    po[s] = ok ? st.pout[(size_t)c * nst + t] : 0.0;
-    const double zz = ok ? st.z[(size_t)c * nst + t] : 0.0;
+    al[s] = ok ? arow[t] : 1.0;
+    po[s] = ok ? prow[t] : 0.0;
+    const double zz = ok ? zrow[t] : 0.0;
     zb |= (zz != 0.0) ? (1u << s) : 0u;
     yv[s] = 0.0;
   }
+  auto RR = [&](int s) __attribute__((always_inline)) -> double { return md.resid[64 * s + lane]; };
+  auto S2 = [&](int s) __attribute__((always_inline)) -> double { return md.sig2[64 * s + lane]; };
   int status = 0;
   lds_order();
 
@@ -571,7 +691,7 @@ __global__ void __launch_bounds__(64 * WPB)
 #pragma unroll
     for (int s = 0; s < NS; ++s) tb[s] = 0.0;
     const int nsl = md.nslot_toa;
-    const double* tc = md.Tcol + lane;
+    const double* tc = md.Tcol;
     int j = 0;
 #pragma unroll 1
     for (; j + 8 <= m; j += 8) {
@@ -580,8 +700,8 @@ __global__ void __launch_bounds__(64 * WPB)
       for (int u = 0; u < 8; ++u) {
 #pragma unroll
         for (int s = 0; s < NS; ++s)
-          tv[u][s] = tc[(size_t)(j + u) * npad + 64 * (s < nsl ? s : nsl - 1)];
-        bj[u] = bbuf[j + u];
+          tv[u][s] = tc[(j + u) * npad + 64 * (s < nsl ? s : nsl - 1) + lane];
+        bj[u] = bsc[j + u];
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u)
@@ -590,13 +710,13 @@ __global__ void __launch_bounds__(64 * WPB)
     }
 #pragma unroll 1
     for (; j < m; ++j) {
-      const double bjj = bbuf[j];
+      const double bjj = bsc[j];
 #pragma unroll
       for (int s = 0; s < NS; ++s)
-        tb[s] = fma(tc[(size_t)j * npad + 64 * (s < nsl ? s : nsl - 1)], bjj, tb[s]);
+        tb[s] = fma(tc[j * npad + 64 * (s < nsl ? s : nsl - 1) + lane], bjj, tb[s]);
     }
 #pragma unroll
-    for (int s = 0; s < NS; ++s) yv[s] = (s < nsl) ? rr[s] - tb[s] : 0.0;
+    for (int s = 0; s < NS; ++s) yv[s] = (s < nsl) ? RR(s) - tb[s] : 0.0;
   };
 
   // sum of log-priors (gibbs.py:337-339): every prior is uniform, so the sum is the
@@ -627,6 +747,9 @@ __global__ void __launch_bounds__(64 * WPB)
     for (int s = 0; s < NS; ++s)
       if ((vmask >> s) & 1u) la += ((zb >> s) & 1u) ? log(al[s]) : 0.0;
     wcls_la = wave_sum(la);
+    int cls[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) cls[s] = md.cidx[64 * s + lane];
     for (int u = 0; u < md.ncls; ++u) {
       double w = 0.0;
 #pragma unroll
@@ -658,7 +781,7 @@ __global__ void __launch_bounds__(64 * WPB)
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       if (vmask & (1u << s)) {
-        const double N0 = ef2 * s2[s] + Q;
+        const double N0 = ef2 * S2(s) + Q;
         const double N = ((zb >> s) & 1u ? al[s] : 1.0) * N0;
         sl += log(N);
         sq += yv[s] * yv[s] / N;
@@ -704,10 +827,11 @@ __global__ void __launch_bounds__(64 * WPB)
                            md.mh_size[2] * (cnt == 2) + md.mh_size[3] * (cnt == 3) +
                            md.mh_size[4] * (cnt == 4);
       const double delta = mh_step(xi, white ? md.sig_w : md.sig_h, scale);
-      mhv[4 * lane + 0] = par;
-      mhv[4 * lane + 1] = delta;
-      mhv[4 * lane + 2] = la;
-      mhv[4 * lane + 3] = exp(2.0 * delta * 2.302585092994045684);
+      double* e = white ? mhw + 4 * step : mhh + 4 * step;
+      e[0] = par;
+      e[1] = delta;
+      e[2] = la;
+      e[3] = exp(2.0 * delta * 2.302585092994045684);
     }
     lds_order();
   };
@@ -716,12 +840,13 @@ __global__ void __launch_bounds__(64 * WPB)
   // returns log(u_accept).  E receives 10^(2 delta) (equad moves rescale Q by it).
   auto propose = [&](const double (&xq)[4], double (&qv)[4], int gs, double& E, int& par)
       __attribute__((always_inline)) -> double {
-    par = (int)mhv[4 * gs + 0];
-    const double delta = mhv[4 * gs + 1];
-    E = mhv[4 * gs + 3];
+    const double* e = gs < NWHITE ? mhw + 4 * gs : mhh + 4 * (gs - NWHITE);
+    par = (int)e[0];
+    const double delta = e[1];
+    E = e[3];
 #pragma unroll
     for (int j = 0; j < 4; ++j) qv[j] = (j == par) ? xq[j] + delta : xq[j];
-    return mhv[4 * gs + 2];
+    return e[2];
   };
 
   // ---------------- matrix state ----------------
@@ -741,9 +866,10 @@ __global__ void __launch_bounds__(64 * WPB)
       const int t = 64 * s + lane;
       double w = 0.0;
       if (vmask & (1u << s)) {
-        const double N = ((zb >> s) & 1u ? al[s] : 1.0) * (ef2 * s2[s] + Q);
+        const double N = ((zb >> s) & 1u ? al[s] : 1.0) * (ef2 * S2(s) + Q);
         sl += log(N);
-        sr += rr[s] * rr[s] / N;
+        const double rs = RR(s);
+        sr += rs * rs / N;
         w = 1.0 / N;
       }
       vbuf[t] = w;
@@ -760,9 +886,9 @@ __global__ void __launch_bounds__(64 * WPB)
     // its MFMAs have issued, so a T load has two k-steps (30 MFMAs) to arrive from L2
     double ta[NT], tb[NT], wa, wb;
     auto tload = [&](double (&t)[NT], double& w, int ks) __attribute__((always_inline)) {
-      const double* src = md.Tmf + (size_t)ks * NT * 64 + lane;
+      const double* src = md.Tmf + (size_t)ks * NT * 64;
 #pragma unroll
-      for (int X = 0; X < NT; ++X) t[X] = src[X * 64];
+      for (int X = 0; X < NT; ++X) t[X] = src[X * 64 + lane];
       w = vbuf[4 * ks + tl];
     };
     auto kstep = [&](const double (&t)[NT], const double wt) __attribute__((always_inline)) {
@@ -813,9 +939,9 @@ __global__ void __launch_bounds__(64 * WPB)
       const int j = 8 * s + q;
       if (p == q) L[SL(s, s)] = (j < md.ntm) ? L[SL(s, s)] + md.tm_phiinv : 1.0;
     }
-    CholCtx cc{colq, lane, p, q, raug, 1.0, 0.0, 0, 0, {1.0, 1.0}, {0.0, 0.0}};
+    CholCtx cc{colq, phbuf, lane, p, q, raug, 1.0, 0.0, 0, 0, {1.0, 1.0}, {0.0, 0.0}};
     GST_SUB_END(10)
-    chol_range<MT, 0, 8 * K0>(L, cc);
+    chol_range_lean<MT, 0, 8 * K0>(L, cc);
     chol_harvest<MT, 0, 8 * K0, RA>(L, cc);
     chol_stats<0, 8 * K0>(cc);
     GST_SUB_END(11)
@@ -829,6 +955,11 @@ __global__ void __launch_bounds__(64 * WPB)
     for (int r = K0; r < MT; ++r)
 #pragma unroll
       for (int s = K0; s <= r; ++s) S0[64 * SL(r - K0, s - K0)] = L[SL(r, s)];
+    // the frozen timing-model columns: parked in global scratch until the b draw
+#pragma unroll
+    for (int s = 0; s < K0; ++s)
+#pragma unroll
+      for (int r = s; r < MT; ++r) tmf[64 * tm_slot(MT, r, s) + lane] = L[SL(r, s)];
   };
 
   // b-marginalised likelihood at xq (gibbs.py:288-329); factor left in L.
@@ -839,7 +970,10 @@ __global__ void __launch_bounds__(64 * WPB)
     // log phi_k = 2 lA ln10 - log(12 pi^2) + (g-3) log fyr - g log f_k + log df_k
     const double lc = 2.0 * lA * 2.302585092994045684 - md.log_12pi2 + (g - 3.0) * md.log_fyr;
     for (int f = lane; f < md.nf; f += 64)
-      phbuf[md.ntm_pad + f] = exp(-(lc - g * lfq[f] + ldq[f]));
+      phbuf[md.ntm_pad + f] = exp(-(lc - g * md.lfreq[f] + md.ldf[f]));
+    // phbuf doubles as the eliminations' junk rows: restore the one other entry read
+    // below, the augmented row's (no prior on the residual column)
+    if (lane == 63) phbuf[raug] = 0.0;
     // sum_k log phi_k in closed form (no reduction on the critical path)
     const double logdet_phi =
         ((double)md.nf * lc - g * md.sum_lfreq + md.sum_ldf) + md.logdet_phi_tm;
@@ -852,7 +986,7 @@ __global__ void __launch_bounds__(64 * WPB)
         if (r == s && p == q) v += phbuf[8 * r + p];
         L[SL(r, s)] = v;
       }
-    CholCtx cc{colq, lane, p, q, raug, 1.0, 0.0, 0, 0, {tm_apr, 1.0}, {tm_zr, 0.0}};
+    CholCtx cc{colq, phbuf, lane, p, q, raug, 1.0, 0.0, 0, 0, {tm_apr, 1.0}, {tm_zr, 0.0}};
     GST_SUB_END(7)
     chol_range<MT, K0, RA>(L, cc);
     chol_harvest<MT, 8 * K0, RA, RA>(L, cc);
@@ -890,7 +1024,7 @@ __global__ void __launch_bounds__(64 * WPB)
         const size_t base = (size_t)c * rec.nrec + ri;
         if (rec.x && lane < P) rec.x[base * P + lane] = pget(xv, lane);
         if (rec.b)
-          for (int j = lane; j < m; j += 64) rec.b[base * m + j] = bbuf[j];
+          for (int j = lane; j < m; j += 64) rec.b[base * m + j] = bsc[j];
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
           const int t = 64 * s + lane;
@@ -958,11 +1092,11 @@ __global__ void __launch_bounds__(64 * WPB)
           for (int i = 0; i < j; ++i) {
             if ((b >> i) & 1) {
               const int gs = s0 + i;
-              const int par = (int)mhv[4 * gs + 0];
-              const double delta = mhv[4 * gs + 1];
+              const int par = (int)mhw[4 * gs + 0];
+              const double delta = mhw[4 * gs + 1];
 #pragma unroll
               for (int t = 0; t < 4; ++t) xq[t] = (t == par) ? xq[t] + delta : xq[t];
-              if (par == md.idx_equad) Q = Q * mhv[4 * gs + 3];
+              if (par == md.idx_equad) Q = Q * mhw[4 * gs + 3];
             }
           }
           double qv[4], E;
@@ -978,7 +1112,7 @@ __global__ void __launch_bounds__(64 * WPB)
           const int L = (1 << jj) - 1 + path;
           const double pl = rdlane(p1, L);
           const double ll = rdlane(l1, L);
-          const double luacc = mhv[4 * (s0 + jj) + 2];
+          const double luacc = mhw[4 * (s0 + jj) + 2];
           if (pl != -INFINITY && (ll + pl) - (l0 + p0) > luacc) {
             l0 = ll;
             p0 = pl;
@@ -990,11 +1124,11 @@ __global__ void __launch_bounds__(64 * WPB)
         for (int i = 0; i < nd; ++i) {
           if ((path >> i) & 1) {
             const int gs = s0 + i;
-            const int par = (int)mhv[4 * gs + 0];
-            const double delta = mhv[4 * gs + 1];
+            const int par = (int)mhw[4 * gs + 0];
+            const double delta = mhw[4 * gs + 1];
 #pragma unroll
             for (int t = 0; t < 4; ++t) xv[t] = (t == par) ? xv[t] + delta : xv[t];
-            if (par == md.idx_equad) Qx = Qx * mhv[4 * gs + 3];
+            if (par == md.idx_equad) Qx = Qx * mhw[4 * gs + 3];
           }
         }
       }
@@ -1112,6 +1246,10 @@ __global__ void __launch_bounds__(64 * WPB)
         status |= 2;
       } else {
         GST_SUB_BEGIN
+#pragma unroll
+        for (int s = 0; s < K0; ++s)
+#pragma unroll
+          for (int r = s; r < MT; ++r) L[SL(r, s)] = tmf[64 * tm_slot(MT, r, s) + lane];
         // y_k = 1/sqrt(a_kk); z = L^-1 d has z_k = zraw_k * y_k; L_ik = a_ik * y_k
 #pragma unroll
         for (int sl = 0; sl < 2; ++sl) {
@@ -1146,8 +1284,14 @@ __global__ void __launch_bounds__(64 * WPB)
             if (p == 0 && j < raug) wvec[j] = (zraw[j] + part) * yinv[j];
           }
         } else {
-          for (int j = lane; j < raug; j += 64)
-            wvec[j] = zraw[j] * yinv[j] + normal_from(rng, (uint32_t)j, TAG_BDRAW);
+          // normals 2l and 2l + 1 of the b-draw stream from lane l's one Philox draw
+          if (2 * lane < raug) {
+            double n0, n1;
+            normal_pair(rng, (uint32_t)lane, TAG_BDRAW, n0, n1);
+            const int j0 = 2 * lane, j1 = 2 * lane + 1;
+            wvec[j0] = zraw[j0] * yinv[j0] + n0;
+            if (j1 < raug) wvec[j1] = zraw[j1] * yinv[j1] + n1;
+          }
         }
         lds_order();
         GST_SUB_END(12)
@@ -1172,11 +1316,11 @@ __global__ void __launch_bounds__(64 * WPB)
           acc += __shfl_xor(acc, 16, 64);
           acc += __shfl_xor(acc, 32, 64);
           // diagonal block, transposed through LDS: dcol[i] = a_{8K+i, 8K+q}
-          tbuf[8 * q + p] = L[SL(K, K)];
+          tdg[8 * q + p] = L[SL(K, K)];
           lds_order();
           double dcol[8];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) dcol[i] = tbuf[8 * q + i];
+          for (int i = 0; i < 8; ++i) dcol[i] = tdg[8 * q + i];
           const int kq = 8 * K + q;
           const double wq = wvec[kq], yq = yinv[kq];
           lds_order();
@@ -1196,7 +1340,11 @@ __global__ void __launch_bounds__(64 * WPB)
         }
         lds_order();
         GST_SUB_END(13)
-        for (int j = lane; j < m; j += 64) bbuf[j] = xbuf[md.ref2int[j]];
+        for (int j = lane; j < m; j += 64) {
+          const double bj = xbuf[md.ref2int[j]];
+          bsc[j] = bj;
+          brow[j] = bj;                   // the state array is the chain's b
+        }
         lds_order();
         compute_Tb();
         GST_SUB_END(14)
@@ -1217,8 +1365,9 @@ __global__ void __launch_bounds__(64 * WPB)
       if (TAPE) {
         theta = tp[TP_DELTA + m];
       } else {
-        const double ga = gamma_mt(a, rng, 0u, TAG_THETA);
-        const double gb = gamma_mt(b, rng, 1u, TAG_THETA);
+        // Gamma(a) on lane 0, Gamma(b) on lane 1 (and its copies), side by side
+        const double g = gamma_mt(lane == 0 ? a : b, rng, lane == 0 ? 0u : 1u, TAG_THETA);
+        const double ga = rdlane(g, 0), gb = rdlane(g, 1);
         theta = ga / (ga + gb);
       }
     }
@@ -1229,7 +1378,7 @@ __global__ void __launch_bounds__(64 * WPB)
       for (int s = 0; s < NS; ++s) {
         if (vmask & (1u << s)) {
           const int t = 64 * s + lane;
-          const double N0 = ef2 * s2[s] + Q;
+          const double N0 = ef2 * S2(s) + Q;
           const double Nv = al[s] * N0;
           const double y = yv[s];
           const double sd1 = sqrt(Nv);
@@ -1266,7 +1415,7 @@ __global__ void __launch_bounds__(64 * WPB)
           if (vmask & (1u << s)) {
             const int t = 64 * s + lane;
             const double zf = (double)((zb >> s) & 1u);
-            const double N0 = ef2 * s2[s] + Q;
+            const double N0 = ef2 * S2(s) + Q;
             const double top = ((yv[s] * yv[s]) * zf / N0 + nu) / 2.0;
             double G;
             if (TAPE) {
@@ -1333,15 +1482,14 @@ __global__ void __launch_bounds__(64 * WPB)
   GST_STAMP(6)
   GST_STAMP_FLUSH
   // ---------------- write back ----------------
-  if (lane < P) st.x[(size_t)c * P + lane] = pget(xv, lane);
-  for (int j = lane; j < m; j += 64) st.b[(size_t)c * m + j] = bbuf[j];
+  if (lane < P) xrow[lane] = pget(xv, lane);
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const int t = 64 * s + lane;
     if (vmask & (1u << s)) {
-      st.z[(size_t)c * nst + t] = (double)((zb >> s) & 1u);
-      st.alpha[(size_t)c * nst + t] = al[s];
-      st.pout[(size_t)c * nst + t] = po[s];
+      zrow[t] = (double)((zb >> s) & 1u);
+      arow[t] = al[s];
+      prow[t] = po[s];
     }
   }
   if (lane == 0) {

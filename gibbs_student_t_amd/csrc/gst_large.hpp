@@ -713,7 +713,7 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
   } else {
     for (int k = tid; k < nf; k += LBLK)
       wv_[k] = S[nf * SS + k] * rsqrt_nr(S[k * SS + k]) +
-               normal_from(rng, (uint32_t)(K0 + k), TAG_BDRAW);
+               normal_k(rng, (uint32_t)(K0 + k), TAG_BDRAW);
   }
   __syncthreads();
   for (int k = tid; k < nf; k += LBLK) vv[k] = 0.0;   // acc_k = sum_{i>k} a_ik v_i
@@ -772,7 +772,7 @@ __global__ void __launch_bounds__(LBLK) lg_btm(const DevModel* __restrict__ mds,
   } else {
     for (int k = tid; k < K0; k += LBLK)
       wk[k] = Gc[(size_t)raug * mp + k] * rsqrt_nr(Gc[(size_t)k * mp + k]) +
-              normal_from(rng, (uint32_t)k, TAG_BDRAW);
+              normal_k(rng, (uint32_t)k, TAG_BDRAW);
   }
   __syncthreads();
   for (int i = K0 - 1; i >= 0; --i) {

@@ -32,3 +32,10 @@ def test_rhat_detects_disagreeing_chains():
 
 def test_constant_chain_is_nan():
     assert np.isnan(diag.bulk_ess(np.ones((4, 100))))
+
+
+def test_ess_rhat_equals_separate_functions():
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal((6, 200)).cumsum(axis=1) * 0.1 + rng.standard_normal((6, 200))
+    e, r = diag.ess_rhat(x)
+    assert e == diag.bulk_ess(x) and r == diag.split_rhat(x)
