@@ -117,7 +117,26 @@ kfn_t pick(int MT, int NS, int K0, int RA, bool tape, int wpb, bool occ2) {
   GST_CASE(10, 2, 2, 76)   // J1713-like, n <= 128 (no_outlier datasets)
   GST_CASE(10, 3, 2, 76)   // J1713+0747: n = 130, 30 red-noise components, 14 TM columns
   GST_CASE(10, 4, 2, 76)   // n <= 256
+  GST_CASE(8, 2, 2, 56)    // <= 20 red-noise components, <= 16 TM columns
+  GST_CASE(8, 3, 2, 56)
+  GST_CASE(8, 4, 2, 56)
+  GST_CASE(10, 2, 3, 76)   // <= 26 components with 17..24 TM columns
+  GST_CASE(10, 3, 3, 76)
+  GST_CASE(10, 4, 3, 76)
 #undef GST_CASE
+  return nullptr;
+}
+
+// Register-resident shapes (MT, K0, RA), smallest first: a model with nf Fourier and ntm
+// timing-model columns runs in the first with 8 K0 >= ntm and RA - 8 K0 >= nf, padded.
+struct Shape {
+  int MT, K0, RA;
+};
+const Shape kShapes[] = {{8, 2, 56}, {10, 2, 76}, {10, 3, 76}};
+
+const Shape* shape_for(int nf, int ntm) {
+  for (const Shape& sh : kShapes)
+    if (8 * sh.K0 >= (ntm > 0 ? ntm : 1) && sh.RA - 8 * sh.K0 >= nf) return &sh;
   return nullptr;
 }
 
@@ -167,10 +186,12 @@ int gst_ctx_destroy(void* ctx) {
 }
 
 // Pack one dataset's constants (shapes already validated) into device buffers owned by cx.
-static int pack_dataset(Ctx* cx, const gst_model_desc* d, gst::DevModel& md, int tm_align) {
+// ntm_pad / raug: the internal positions of the first Fourier column and of the residual
+// row; a persistent-kernel instance larger than the model leaves unit-prior dummy columns
+// between the Fourier block and the residual row.
+static int pack_dataset(Ctx* cx, const gst_model_desc* d, gst::DevModel& md, int ntm_pad,
+                        int raug) {
   const int n = d->n, m = d->m, nf = d->nfourier, ntm = d->ntm, P = d->nparams;
-  const int ntm_pad = round_up(ntm > 0 ? ntm : 1, tm_align);
-  const int raug = ntm_pad + nf;
   const int mpad = round_up(raug + 1, 16);
   const int npad = 64 * ((n + 63) / 64);
 
@@ -374,13 +395,12 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
   }
   const gst_model_desc* d = &descs[0];
   const int nf = d->nfourier, ntm = d->ntm, m = d->m;
-  const int ntm_pad = round_up(ntm > 0 ? ntm : 1, 8);
-  const int raug = ntm_pad + nf;
-  const int mpad = round_up(raug + 1, 16);
-  const int MT = mpad / 8, K0 = ntm_pad / 8;
+  const Shape* sh = shape_for(nf, ntm);
+  const int MT = sh ? sh->MT : 0, K0 = sh ? sh->K0 : 0;
+  const int raug = sh ? sh->RA : 0;
   const int nsl = (nmax + 63) / 64;
   const int NS = nsl <= 2 ? 2 : (nsl <= 3 ? 3 : 4);
-  const bool fits = round_up(nmax, 4) <= 64 * NS && pick(MT, NS, K0, raug, false, 4, false);
+  const bool fits = sh && round_up(nmax, 4) <= 64 * NS && pick(MT, NS, K0, raug, false, 4, false);
   int path = cx->path_req;
   if (path == GST_PATH_AUTO) path = fits ? GST_PATH_PERSISTENT : GST_PATH_LARGE;
   if (path == GST_PATH_PERSISTENT && !fits) {
@@ -398,10 +418,12 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
       return fail("gst_model_set: large path needs nfourier <= 138 (LDS-resident Fourier block)");
   }
   free_model(cx);
-  const int tm_align = path == GST_PATH_LARGE ? 16 : 8;
+  // large path: timing-model block padded to whole 16-column MFMA tiles, no dummies
+  const int ntm_pad = path == GST_PATH_LARGE ? round_up(ntm > 0 ? ntm : 1, 16) : 8 * K0;
+  const int raug_pack = path == GST_PATH_LARGE ? ntm_pad + nf : raug;
   std::vector<gst::DevModel> hmd(nd);
   for (int i = 0; i < nd; ++i)
-    if (pack_dataset(cx, &descs[i], hmd[i], tm_align)) {
+    if (pack_dataset(cx, &descs[i], hmd[i], ntm_pad, raug_pack)) {
       free_model(cx);
       return -1;
     }

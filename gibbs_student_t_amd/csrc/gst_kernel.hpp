@@ -969,8 +969,10 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     const double g = pget(xq, md.idx_gamma);
     // log phi_k = 2 lA ln10 - log(12 pi^2) + (g-3) log fyr - g log f_k + log df_k
     const double lc = 2.0 * lA * 2.302585092994045684 - md.log_12pi2 + (g - 3.0) * md.log_fyr;
-    for (int f = lane; f < md.nf; f += 64)
-      phbuf[md.ntm_pad + f] = exp(-(lc - g * md.lfreq[f] + md.ldf[f]));
+    // Fourier columns, then the unit-prior dummies that pad a smaller model up to this
+    // instance's RA (zero Gram rows: each is eliminated as an exact no-op)
+    for (int f = lane; f < RA - md.ntm_pad; f += 64)
+      phbuf[md.ntm_pad + f] = f < md.nf ? exp(-(lc - g * md.lfreq[f] + md.ldf[f])) : 1.0;
     // phbuf doubles as the eliminations' junk rows: restore the one other entry read
     // below, the augmented row's (no prior on the residual column)
     if (lane == 63) phbuf[raug] = 0.0;

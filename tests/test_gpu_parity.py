@@ -373,3 +373,17 @@ def test_paths_agree_in_philox_mode():
     for k in ("b", "alpha", "pout", "theta"):
         r = _rel(b[k][same], a[k][same])
         assert np.all(r <= 1e-8), f"{k}: max rel {r.max():.3e}"
+
+
+@pytest.mark.parametrize("name,path", [("c20_beta_fixed", "persistent"),
+                                       ("tm22_beta_fixed", "persistent"),
+                                       ("beta_fixed", "persistent"),
+                                       ("scaled_beta_fixed", "large")])
+def test_auto_path_choice(name, path):
+    """Register-resident instances cover <= 20 components (MT 8), <= 30 with <= 16 TM
+    columns and <= 26 with 17..24 TM columns (MT 10), padded with unit-prior dummies;
+    larger models take the large path."""
+    ref = load_ref(name)
+    ns = NativeSampler(ref["pta"], ref["kw"], 0)
+    assert ns.path == path
+    ns.close()

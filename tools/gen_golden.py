@@ -341,8 +341,44 @@ def configs34(niter=12):
                   file=sys.stderr)
 
 
+def shapes(niter=12):
+    """Other model shapes on the J1713+0747 epochs (register-resident instances padded with
+    unit-prior dummy columns):
+
+    * ``c20``: 20 red-noise components (the notebook's count, gibbs_likelihood.ipynb cell 2)
+      with the 14 timing-model columns;
+    * ``tm22``: 20 components with 22 timing-model columns (the 14 plus 8 DMX-like
+      piecewise-constant offsets over the 5 years), i.e. 17..24 columns -> 3 TM panels.
+    """
+    import copy
+    psr = gdata.j1713(seed=1713, theta=0.05)
+    pta_a = PTA(psr, components=20)
+    np.savez_compressed(os.path.join(OUTDIR, "c20_dataset.npz"), **dataset_arrays(pta_a, psr))
+    psr22 = copy.deepcopy(psr)
+    t = psr.toas
+    edges = np.linspace(t.min(), t.max() + 1.0, 9)
+    dmx = np.stack([((t >= a) & (t < b)).astype(float) for a, b in zip(edges[:-1], edges[1:])],
+                   axis=1)
+    psr22.Mmat = np.column_stack([psr.Mmat, dmx])
+    pta_b = PTA(psr22, components=20)
+    assert pta_b.ntm == 22, pta_b.ntm
+    np.savez_compressed(os.path.join(OUTDIR, "tm22_dataset.npz"), **dataset_arrays(pta_b, psr22))
+    for tag, pta_s, models in (("c20", pta_a, ("beta", "t", "vvh17")),
+                               ("tm22", pta_b, ("beta", "uniform"))):
+        for j, name in enumerate(models):
+            out = run_one(pta_s, name, MODELS[name], seed=6100 + 17 * j + len(tag),
+                          niter=niter, x0=[4.33, -14.0, -7.6])
+            out["model_kw"] = np.array(repr(MODELS[name]))
+            np.savez_compressed(os.path.join(OUTDIR, f"ref_{tag}_{name}_fixed.npz"), **out)
+            print(tag, name, "m", pta_s.m, "cond:", np.nanmax(out["tape_b_cond"]),
+                  file=sys.stderr)
+
+
 def main():
     os.makedirs(OUTDIR, exist_ok=True)
+    if "--only-shapes" in sys.argv:
+        shapes(12)
+        return
     niter = 12
     if "--only-simclean" in sys.argv:
         simclean(niter)
@@ -396,6 +432,7 @@ def main():
     simclean(niter)
     scaled()
     configs34(niter)
+    shapes(niter)
 
 
 if __name__ == "__main__":
