@@ -412,7 +412,6 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
     return fail(b);
   }
   if (path == GST_PATH_LARGE) {
-    if (nd != 1) return fail("gst_model_set: the large path takes one dataset per context");
     const int ms = nf + 1;
     if ((size_t)(ms * (ms + 1) + nf + 2 * ms) * 8 > 160 * 1024)
       return fail("gst_model_set: large path needs nfourier <= 138 (LDS-resident Fourier block)");
@@ -500,11 +499,18 @@ static int ev_mark(Ctx* cx, int kind, hipStream_t st, bool begin) {
     if (ev_mark(cx, kind, st, false)) return -1;                                 \
   } while (0)
 
+// per-TOA scratch row stride of the large path: the batch's largest npad
+static int large_ys(const Ctx* cx) {
+  int ys = 0;
+  for (const gst::DevModel& h : cx->hmd) ys = std::max(ys, h.npad);
+  return ys;
+}
+
 static int ensure_scratch(Ctx* cx, int C) {
   if (C <= cx->scratch_C) return 0;
   free_scratch(cx);
   const gst::DevModel& h = cx->hmd[0];
-  const size_t mp = h.mp, npad = h.npad;
+  const size_t mp = h.mp, npad = large_ys(cx);
   HIP_OK(hipMalloc(&cx->ls.G, (size_t)C * mp * mp * 8));
   HIP_OK(hipMalloc(&cx->ls.y, (size_t)C * npad * 8));
   HIP_OK(hipMalloc(&cx->ls.w, (size_t)C * npad * 8));
@@ -524,13 +530,14 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
                         hipStream_t st) {
   if (ensure_scratch(cx, C)) return -1;
   const gst::DevModel& h = cx->hmd[0];
-  gst::LArgs a{ds, dr, dt, cx->ls, C, nsweeps, 0, record_every, mask, seed, sweep0, chain0,
+  const int ys = large_ys(cx);
+  gst::LArgs a{ds, dr, dt, cx->ls, ys, C, nsweeps, 0, record_every, mask, seed, sweep0, chain0,
                eval_only, ow, oh};
   const int nsb = (h.mp / 16 + 3) / 4;
   const int npairs = nsb * (nsb + 1) / 2;
   const dim3 g_chain(C), b_chain(gst::LBLK), b_toa(gst::TBLK);
   const dim3 g_gram(npairs * ((C + gst::GRAM_WAVES - 1) / gst::GRAM_WAVES)), b_gram(64 * gst::GRAM_WAVES);
-  const dim3 g_tb(h.npad / 64, (C + 63) / 64);
+  const dim3 g_tb(ys / 64, (C + 63) / 64);
   cx->evused = 0;
   HIP_OK(hipEventRecord(cx->ev0, st));
   LG_LAUNCH(GST_K_TB, gst::lg_tb, g_tb, b_chain, 0);   // y = r - T b for the current b

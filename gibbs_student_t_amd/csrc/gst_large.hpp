@@ -58,6 +58,7 @@ struct LArgs {
   DevRec rec;
   DevTape tape;
   LScratch s;
+  int ys;  // row stride of the per-TOA scratch y, w: the batch's largest npad
   int C, nsweeps, it, record_every;
   unsigned mask;
   unsigned long long seed;
@@ -65,6 +66,16 @@ struct LArgs {
   int eval_only;
   double *out_w, *out_h;
 };
+
+// Dataset of chain c (dataset batches: one DevModel per dataset).  Chains of one 16-chain
+// group must share their dataset (the Gram workgroups and the T b GEMM stage one dataset's
+// T for the whole group; NativeSampler.alloc checks this).  An index out of range reads
+// dataset 0 and is flagged by lg_white (status bit 4).
+constexpr int LGROUP = 16;
+__device__ __forceinline__ int ds_of(const LArgs& a, int c) {
+  const int d = a.st.dataset ? __builtin_amdgcn_readfirstlane(a.st.dataset[c]) : 0;
+  return (unsigned)d < (unsigned)a.st.nd ? d : 0;
+}
 
 __device__ __forceinline__ Rng make_rng(const LArgs& a, int c) {
   Rng r;
@@ -182,7 +193,7 @@ __device__ __forceinline__ void load_x(const DevModel& md, const DevState& st, i
 // ------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(LBLK) lg_record(const DevModel* __restrict__ mds, LArgs a) {
   const int c = blockIdx.x;
-  const DevModel& md = mds[0];
+  const DevModel& md = mds[ds_of(a, c)];
   const int ri = a.it / a.record_every;
   if (ri >= a.rec.nrec) return;
   const size_t base = (size_t)c * a.rec.nrec + ri;
@@ -207,14 +218,17 @@ __global__ void __launch_bounds__(LBLK) lg_record(const DevModel* __restrict__ m
 // ------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(TBLK) lg_white(const DevModel* __restrict__ mds, LArgs a) {
   const int c = blockIdx.x;
-  const DevModel& md = mds[0];
+  const DevModel& md = mds[ds_of(a, c)];
+  if (threadIdx.x == 0 && a.st.dataset && a.st.status &&
+      (unsigned)a.st.dataset[c] >= (unsigned)a.st.nd)
+    a.st.status[c] |= 4;                          // bad dataset index (ran on dataset 0)
   __shared__ double red[TBLK / 64];
   __shared__ double mhv[NWHITE][4];
   const int n = md.n, nst = a.st.nst, npad = md.npad;
   const double* zc = a.st.z + (size_t)c * nst;
   const double* alc = a.st.alpha + (size_t)c * nst;
-  const double* yc = a.s.y + (size_t)c * npad;
-  double* wc = a.s.w + (size_t)c * npad;
+  const double* yc = a.s.y + (size_t)c * a.ys;
+  double* wc = a.s.w + (size_t)c * a.ys;
   double* sc = a.s.sc + (size_t)c * 16;
   double xv[4];
   load_x(md, a.st, c, xv);
@@ -322,7 +336,7 @@ __device__ __forceinline__ void gram_tile(const DevModel& md, const LArgs& a, do
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int NT = md.mp / 16;
   const int nch = md.npad / (4 * GRAM_KC);
-  const double* wc = a.s.w + (size_t)c * md.npad;
+  const double* wc = a.s.w + (size_t)c * a.ys;
   const int tl = lane >> 4;
 
   // staging map: 512 threads x 8 double2 = 8 tiles x 16 k-steps x 32 double2
@@ -424,7 +438,6 @@ __device__ __forceinline__ void gram_tile(const DevModel& md, const LArgs& a, do
 
 __global__ void __launch_bounds__(64 * GRAM_WAVES) lg_gram(const DevModel* __restrict__ mds,
                                                            LArgs a, int nsb, int npairs) {
-  const DevModel& md = mds[0];
   extern __shared__ double lsm[];
   double* Tl = lsm;                               // [2][KC][8 tiles][64]
   double* Wl = lsm + 2 * GRAM_KC * 8 * 64;        // [2][8 waves][64]
@@ -436,6 +449,11 @@ __global__ void __launch_bounds__(64 * GRAM_WAVES) lg_gram(const DevModel* __res
   const int cg = (blockIdx.x % ngroups) * GRAM_WAVES + wv;
   const bool live = cg < a.C;
   const int c = live ? cg : a.C - 1;              // dead waves still stage and sync
+  // the group's dataset (its first chain's): every wave stages that dataset's T
+  const int dsg = ds_of(a, (blockIdx.x % ngroups) * GRAM_WAVES);
+  const DevModel& md = mds[dsg];
+  if (live && prank == 0 && ds_of(a, c) != dsg && (threadIdx.x & 63) == 0 && a.st.status)
+    a.st.status[c] |= 8;                          // batch layout violated: flag, never silent
   const int noff = npairs - nsb;
   int I, J;
   if (prank < noff) {                              // (I, J), I > J, row-major
@@ -472,7 +490,7 @@ __global__ void __launch_bounds__(64 * GRAM_WAVES) lg_gram(const DevModel* __res
 // trailing lower triangle is updated by MFMA: G_ij -= sum_kk P_i,kk P_j,kk / a_kk.
 __global__ void __launch_bounds__(LBLK) lg_tmelim(const DevModel* __restrict__ mds, LArgs a) {
   const int c = blockIdx.x;
-  const DevModel& md = mds[0];
+  const DevModel& md = mds[ds_of(a, c)];
   extern __shared__ double lsm[];
   constexpr int PS = TM_PW + 1;        // panel row stride
   double* P = lsm;                     // [mp][PS]
@@ -560,7 +578,7 @@ struct HyperLds {
 
 __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ mds, LArgs a) {
   const int c = blockIdx.x;
-  const DevModel& md = mds[0];
+  const DevModel& md = mds[ds_of(a, c)];
   extern __shared__ double lsm[];
   const int nf = md.nf, K0 = md.ntm_pad, mp = md.mp;
   const int ms = nf + 1;               // Fourier block + augmented row
@@ -737,7 +755,7 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
 // ------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(LBLK) lg_btm(const DevModel* __restrict__ mds, LArgs a) {
   const int c = blockIdx.x;
-  const DevModel& md = mds[0];
+  const DevModel& md = mds[ds_of(a, c)];
   extern __shared__ double lsm[];
   const int K0 = md.ntm_pad, mp = md.mp, raug = md.raug;
   double* acc = lsm;          // [K0]
@@ -800,12 +818,13 @@ __global__ void __launch_bounds__(LBLK) lg_btm(const DevModel* __restrict__ mds,
 // Wave: 16 chains x 64 TOAs (4 tiles); A = b (chains x basis), B = T^T (basis x TOAs) read
 // from the column-major Tcol so a wave's B fragment is 16 consecutive TOAs.
 __global__ void __launch_bounds__(LBLK) lg_tb(const DevModel* __restrict__ mds, LArgs a) {
-  const DevModel& md = mds[0];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int t0 = blockIdx.x * 64;
   const int cb = (blockIdx.y * 4 + wv) * 16;
   if (cb >= a.C) return;
+  const DevModel& md = mds[ds_of(a, cb)];         // one dataset per 16-chain group
   const int m = md.m, npad = md.npad;
+  if (t0 >= npad) return;                         // beyond this dataset's TOAs
   const int ci = cb + (lane & 15);
   const bool cok = ci < a.C;
   const double* bc = a.st.b + (size_t)(cok ? ci : cb) * m;
@@ -832,7 +851,7 @@ __global__ void __launch_bounds__(LBLK) lg_tb(const DevModel* __restrict__ mds, 
       const int cc = cb + kl + 4 * g;
       const int t = t0 + 16 * u + (lane & 15);
       if (cc < a.C && t < npad)
-        a.s.y[(size_t)cc * npad + t] = (t < md.n) ? md.resid[t] - acc[u][g] : 0.0;
+        a.s.y[(size_t)cc * a.ys + t] = (t < md.n) ? md.resid[t] - acc[u][g] : 0.0;
     }
 }
 
@@ -841,14 +860,14 @@ __global__ void __launch_bounds__(LBLK) lg_tb(const DevModel* __restrict__ mds, 
 // ------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(TBLK) lg_toa(const DevModel* __restrict__ mds, LArgs a) {
   const int c = blockIdx.x;
-  const DevModel& md = mds[0];
+  const DevModel& md = mds[ds_of(a, c)];
   __shared__ double red[TBLK / 64];
   __shared__ double dfb[32];
   const int n = md.n, nst = a.st.nst, m = md.m, tid = threadIdx.x;
   double* zc = a.st.z + (size_t)c * nst;
   double* alc = a.st.alpha + (size_t)c * nst;
   double* poc = a.st.pout + (size_t)c * nst;
-  const double* yc = a.s.y + (size_t)c * md.npad;
+  const double* yc = a.s.y + (size_t)c * a.ys;
   const Rng rng = make_rng(a, c);
   const double* tp = tape_row(a, c);
   double xv[4];

@@ -88,6 +88,27 @@ def split_rhat(x: np.ndarray) -> float:
     return max(bulk, fold)
 
 
+def ess_rhat(x: np.ndarray):
+    """(bulk_ess(x), split_rhat(x)) sharing one rank normalisation of the split chains
+    (the costly step at thousands of chains)."""
+    x = np.asarray(x, dtype=np.float64)
+    if np.all(x == x.flat[0]):
+        return float("nan"), float("nan")
+    s = _split(x)
+    z = _rank_normalise(s)
+
+    def _rhat(y):
+        m, n = y.shape
+        w = y.var(axis=1, ddof=1).mean()
+        b = n * y.mean(axis=1).var(ddof=1)
+        if not w > 0:
+            return float("nan")
+        return float(np.sqrt(((n - 1) / n * w + b / n) / w))
+
+    fold = _rhat(_rank_normalise(np.abs(s - np.median(s))))
+    return ess_raw(z), max(_rhat(z), fold)
+
+
 def ar1_ess(rho: float, m: int, n: int) -> float:
     """Closed-form ESS of m AR(1) chains of length n with coefficient rho (test oracle)."""
     return m * n * (1.0 - rho) / (1.0 + rho)

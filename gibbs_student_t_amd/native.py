@@ -144,6 +144,12 @@ class NativeSampler:
             raise ValueError(f"dataset indices must lie in [0, {self.ndatasets})")
         if dataset is None and self.ndatasets > 1:
             raise ValueError("several datasets: pass dataset= to alloc")
+        if self.path == "large" and self.ndatasets > 1:
+            # the large path stages one dataset's T per 16-chain group (Gram, T b)
+            groups = [ds[i:i + 16] for i in range(0, C, 16)]
+            if any(np.any(grp != grp[0]) for grp in groups):
+                raise ValueError("large path with several datasets: every aligned group of "
+                                 "16 chains must share one dataset")
         self.dataset_host = ds
         self.dataset = torch.as_tensor(ds).to(self.tdev)
         self.state = {

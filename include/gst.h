@@ -87,7 +87,8 @@ typedef struct gst_model_desc {
  * (nmax = largest n of the model's datasets; TOAs t >= n of a chain's dataset are never
  * touched), theta/nu[C]; status[C] may be NULL (bit 0: Cholesky failure seen in the hyper
  * block, bit 1: b-draw factorisation failed and b was kept, bit 2: dataset index out of
- * range -- the chain was not run).  dataset[C] gives each chain's dataset index into the
+ * range -- the persistent path does not run the chain, the large path runs it on dataset
+ * 0; bit 3: large path, the chain's 16-chain group mixes datasets).  dataset[C] gives each chain's dataset index into the
  * batch passed to gst_model_set_batch; it may be NULL when there is one dataset. */
 typedef struct gst_state {
   double* x;
@@ -143,7 +144,9 @@ int gst_model_set(void* ctx, const gst_model_desc* desc);
  * several thetas, each under the five outlier models).  The descriptors must agree in
  * m, nfourier, ntm, nparams, parameter roles and hyper/white index sets; n, the data,
  * priors and the outlier-model options may differ.  Chains pick their dataset through
- * gst_state.dataset. */
+ * gst_state.dataset.  On the large path every aligned group of 16 chains must share one
+ * dataset (its Gram and T b kernels stage one dataset's T per group); a chain whose group
+ * mixes datasets is flagged with status bit 8. */
 int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int ndatasets);
 
 /* Number of datasets, largest n (row stride of per-TOA state/records) and tape stride. */
@@ -168,7 +171,9 @@ int gst_eval_lnlike(void* ctx, const gst_state* state, int nchains, double* out_
 int gst_sync(void* ctx, void* stream);
 
 /* Execution path.  The persistent path keeps a whole chain in one wavefront for all of a
- * launch's sweeps (n <= 256, m <= ~78: J1713+0747-sized pulsars); the large path runs
+ * launch's sweeps (n <= 256 and up to 30 red-noise components with <= 16 timing-model
+ * columns, 26 with <= 24; smaller models run padded with unit-prior dummy columns); the
+ * large path runs
  * each sweep as a pipeline of kernels (fp64-MFMA Gram shared by all chains, blocked
  * timing-model elimination, LDS-resident red-noise MH, MFMA T b, per-TOA passes) for
  * large n and m (BASELINE config 5).  AUTO (default) picks persistent when it fits.

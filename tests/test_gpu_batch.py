@@ -130,3 +130,49 @@ def test_bad_dataset_index_is_flagged():
     assert st["status"][0] == 0 and st["status"][1] == 4
     np.testing.assert_array_equal(st["x"][1], r["xs"])   # untouched
     ns.close()
+
+
+def test_large_path_dataset_batch_equals_single_launches():
+    """The large-model path batches datasets too (ragged n, 16-chain groups per dataset):
+    each chain of a 2-dataset batch is bitwise its dataset's standalone launch."""
+    from gibbs_student_t_amd import data
+    from gibbs_student_t_amd.model import PTA
+    from gibbs_student_t_amd.run_sims import MODELS
+    ptas = [PTA(data.scaled_synthetic(n=n, components=40, ntm=100, seed=sd), components=40)
+            for n, sd in ((1500, 11), (1333, 12))]
+    cfgs = [MODELS["beta"], MODELS["t"]]
+    per, S, seed = 16, 4, 99
+    big = NativeSampler(ptas, cfgs, 0, path="large")
+    assert big.path == "large"
+    with pytest.raises(ValueError):
+        big.alloc(2 * per, dataset=np.tile([0, 1], per))       # groups must not mix
+    big.alloc(2 * per, dataset=np.repeat([0, 1], per))
+    nst = big.n
+
+    def init(pta, c0, width):
+        lo = np.array([p.pmin for p in pta.params])
+        hi = np.array([p.pmax for p in pta.params])
+        x = np.stack([np.random.default_rng([3, c0 + c]).uniform(lo, hi) for c in range(per)])
+        z = np.zeros((per, width))
+        z[:, :pta.n] = 1.0
+        return dict(x=x, b=np.zeros((per, pta.T.shape[1])), z=z, alpha=np.ones((per, width)),
+                    pout=np.zeros((per, width)), theta=np.full(per, 0.01), nu=np.full(per, 4.0))
+
+    parts = [init(p_, d * per, nst) for d, p_ in enumerate(ptas)]
+    big.set_state(**{k: np.concatenate([p[k] for p in parts]) for k in parts[0]})
+    big.sweep(S, seed=seed, sweep0=1)
+    full = big.get_state()
+    assert np.all(full["status"] == 0)
+    for d, (p_, cfg) in enumerate(zip(ptas, cfgs)):
+        one = NativeSampler(p_, cfg, 0, path="large")
+        one.alloc(per)
+        one.set_state(**init(p_, d * per, p_.n))
+        one.sweep(S, seed=seed, sweep0=1, chain0=d * per)
+        o = one.get_state()
+        sl = slice(d * per, (d + 1) * per)
+        for k in ("x", "b", "theta", "nu"):
+            np.testing.assert_array_equal(full[k][sl], o[k], err_msg=f"dataset {d} {k}")
+        for k in ("z", "alpha", "pout"):
+            np.testing.assert_array_equal(full[k][sl][:, :p_.n], o[k], err_msg=f"dataset {d} {k}")
+        one.close()
+    big.close()
