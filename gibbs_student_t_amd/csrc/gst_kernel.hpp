@@ -358,9 +358,9 @@ __device__ __forceinline__ void chol_publish(const double (&L)[SL(MT, 0)], CholC
   double* dst = (cc.q == QQ ? cc.colq : cc.junk) + MT * cc.p;
 #pragma unroll
   for (int r2 = 0; r2 < MT; r2 += 2) {          // rows (r2, r2+1)
-    if (r2 >= s) {
-      dst[r2] = L[SL(r2, s)];
-      dst[r2 + 1] = L[SL(r2 + 1, s)];
+    if (r2 >= s) {  // one ds_write_b128 per row pair (16-byte aligned: MT, r2 even)
+      typedef double v2_t __attribute__((ext_vector_type(2)));
+      *(v2_t*)(dst + r2) = (v2_t){L[SL(r2, s)], L[SL(r2 + 1, s)]};
     } else if (r2 + 1 >= s)
       dst[r2 + 1] = L[SL(r2 + 1, s)];
   }
