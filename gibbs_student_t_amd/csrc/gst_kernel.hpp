@@ -322,6 +322,57 @@ __device__ double gamma_mt(double a, const Rng& rng, uint32_t index, uint32_t ta
   return d * boost;
 }
 
+// gamma_mt for NS draws at once -- draw s with shape a[s] and Philox index index0 + 64 s,
+// for the slots in `active` -- in one rejection loop, so the independent draws' dependency
+// chains interleave.  Every draw consumes exactly gamma_mt's variates in gamma_mt's order,
+// hence returns bitwise gamma_mt(a[s], rng, index0 + 64 s, tag).
+template <int NS>
+__device__ __forceinline__ void gamma_mt_slots(const double (&a)[NS], unsigned active,
+                                               const Rng& rng, uint32_t index0, uint32_t tag,
+                                               double (&out)[NS]) {
+  double d[NS], cc[NS], boost[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    double as = a[s];
+    boost[s] = 1.0;
+    if (((active >> s) & 1u) && as < 1.0) {
+      double ub, unused;
+      rng.uniform2(index0 + 64u * s, tag | 0xFFFFFFu, ub, unused);
+      boost[s] = exp(log(1.0 - ub) / as);
+      as += 1.0;
+    }
+    d[s] = as - 1.0 / 3.0;
+    cc[s] = 1.0 / sqrt(9.0 * d[s]);
+    out[s] = d[s] * boost[s];                 // gamma_mt's value after 256 failed attempts
+  }
+  unsigned pend = active;
+#pragma unroll 1
+  for (uint32_t att = 0; att < 128u && pend; ++att) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (!((pend >> s) & 1u)) continue;
+      double u1, u2, ua, ub;
+      rng.uniform2(index0 + 64u * s, tag | (2u * att), u1, u2);
+      rng.uniform2(index0 + 64u * s, tag | (2u * att + 1u), ua, ub);
+      const double r = sqrt(-2.0 * log(1.0 - u1));
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (!((pend >> s) & 1u)) break;
+        const double xn = r * (h == 0 ? cos2pi(u2) : sin2pi(u2));
+        const double u3 = h == 0 ? ua : ub;
+        double v = 1.0 + cc[s] * xn;
+        if (v <= 0.0) continue;
+        v = v * v * v;
+        const double x2 = xn * xn;
+        if (u3 < 1.0 - 0.0331 * x2 * x2 || log(u3) < 0.5 * x2 + d[s] * (1.0 - v + log(v))) {
+          out[s] = d[s] * v * boost[s];
+          pend &= ~(1u << s);
+        }
+      }
+    }
+  }
+}
+
 // Right-looking LDL^T-scaled Cholesky on the cyclic register layout.
 //
 // Registers keep RAW columns: after column k is eliminated, slot values hold
@@ -1412,20 +1463,26 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
 #pragma unroll
       for (int s = 0; s < NS; ++s) zs += __popcll(__ballot(((zb & vmask) >> s) & 1u));
       if (zs >= 1) {
+        double G[NS];
+        if (TAPE) {
+#pragma unroll
+          for (int s = 0; s < NS; ++s) G[s] = tp[TP_DELTA + m + 1 + nst + 64 * s + lane];
+        } else {
+          // all of the lane's TOAs in one rejection loop (independent draws, so their
+          // Philox / log / sqrt chains interleave); each TOA's variates and acceptance
+          // sequence are exactly gamma_mt's (the large path draws them that way)
+          double sh[NS];
+#pragma unroll
+          for (int s = 0; s < NS; ++s) sh[s] = ((double)((zb >> s) & 1u) + nu) / 2.0;
+          gamma_mt_slots<NS>(sh, vmask, rng, (uint32_t)lane, TAG_ALPHA, G);
+        }
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
           if (vmask & (1u << s)) {
-            const int t = 64 * s + lane;
             const double zf = (double)((zb >> s) & 1u);
             const double N0 = ef2 * S2(s) + Q;
             const double top = ((yv[s] * yv[s]) * zf / N0 + nu) / 2.0;
-            double G;
-            if (TAPE) {
-              G = tp[TP_DELTA + m + 1 + nst + t];
-            } else {
-              G = gamma_mt((zf + nu) / 2.0, rng, (uint32_t)t, TAG_ALPHA);
-            }
-            al[s] = top / G;
+            al[s] = top / G[s];
           }
         }
       }

@@ -28,13 +28,14 @@ GST_HD u32x4 philox4x32_10(u32x4 ctr, uint32_t k0, uint32_t k1) {
   uint32_t c0 = ctr.v[0], c1 = ctr.v[1], c2 = ctr.v[2], c3 = ctr.v[3];
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t hi0 = mulhi32(M0, c0), lo0 = M0 * c0;
-    const uint32_t hi1 = mulhi32(M1, c2), lo1 = M1 * c2;
-    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    // one 32x32 -> 64-bit product per multiplier gives both halves (v_mad_u64_u32 on
+    // gfx950, instead of separate quarter-rate v_mul_hi_u32 + v_mul_lo_u32)
+    const uint64_t p0 = (uint64_t)M0 * c0, p1 = (uint64_t)M1 * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
     c0 = n0;
-    c1 = lo1;
+    c1 = (uint32_t)p1;
     c2 = n2;
-    c3 = lo0;
+    c3 = (uint32_t)p0;
     k0 += W0;
     k1 += W1;
   }
