@@ -472,7 +472,9 @@ def main():
                    "hbm_frac": gbs / HBM_PEAK_GBS,
                    "bytes_per_chain_sweep": toa_pass_bytes(n_eff)}
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        # HBM bytes per chain-sweep of the persistent kernel, PMC (FETCH_SIZE x 2 +
+        # WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction) at 2048 chains, 200 sweeps
+        pmc = os.path.join(ROOT, "profiles", "r2_pmc_config2.json")
         if os.path.exists(pmc) and args.config == 2 and not args.stub:
             try:
                 pj = json.load(open(pmc))
@@ -533,7 +535,8 @@ def main():
                          "executed_flop_per_chain_sweep": exe,
                          "per_toa_pass": toa if toa else
                          "fused into the persistent kernel (no separate launch to time); "
-                         "stage shares in profiles/r2_stages_config2.txt"},
+                         "stage costs from stage-masked launches in "
+                         "profiles/r2_stage_costs_config2.txt"},
             "cpu_baseline": cpu,
         }
         if stages:
