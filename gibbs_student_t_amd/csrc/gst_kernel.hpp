@@ -682,7 +682,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   double* yinv = xbuf + MP;           //   1/sqrt(a_kk)
   double* bsc = yinv + MP;            //   b in reference order (T b input)
   double* tdg = bsc + MP;             //   8 x 8 diagonal-block transposes
-  double* dfbuf = S0R;                // nu grid (32)
+  double* dfbuf = S0R;                // nu grid: weights [32], probabilities [32]
   // the TM factor slots (s < K0) wait in global scratch while the hyper block runs
   // per-chain rows of the state arrays: wave-uniform base pointers (SGPRs), so every
   // per-lane access is base + 32-bit lane offset
@@ -1522,16 +1522,19 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
                    ((acc8[4] + acc8[5]) + (acc8[6] + acc8[7]));
 #pragma unroll
       for (int i = 24; i < 30; ++i) tot += dfbuf[i];
-      double cdf[30];
-      double cs = 0.0;
+      // p_i = e_i / tot on lane i (one division per lane, not 30 per lane), the cumsum in
+      // numpy's sequential order over the published p's (each lane keeps its own prefix),
+      // then lane i tests cdf_i / cdf_29 <= u and the ballot counts (searchsorted 'right')
+      const double pl = lane < 30 ? dfbuf[lane] / tot : 0.0;
+      if (lane < 30) dfbuf[32 + lane] = pl;
+      lds_order();
+      double cs = 0.0, mine = 0.0;
 #pragma unroll
       for (int i = 0; i < 30; ++i) {
-        cs += dfbuf[i] / tot;
-        cdf[i] = cs;
+        cs += dfbuf[32 + i];
+        mine = (i == lane) ? cs : mine;
       }
-      int cnt = 0;
-#pragma unroll
-      for (int i = 0; i < 30; ++i) cnt += (cdf[i] / cdf[29] <= u) ? 1 : 0;
+      int cnt = __popcll(__ballot(lane < 30 && mine / cs <= u));
       cnt = cnt < 29 ? cnt : 29;
       nu = (double)(cnt + 1);
       lds_order();
