@@ -24,7 +24,7 @@ KERNEL_KINDS = ("record", "white", "gram", "tmelim", "hyper", "btm", "tb", "toa"
 ABI_VERSION = 2
 EXPORTS = ("gst_version", "gst_tape_stride", "gst_last_error", "gst_ctx_create",
            "gst_ctx_destroy", "gst_model_set", "gst_model_set_batch", "gst_model_info",
-           "gst_sweep", "gst_set_path", "gst_get_path", "gst_set_timing", "gst_kernel_times", "gst_eval_lnlike", "gst_sync",
+           "gst_sweep", "gst_set_path", "gst_get_path", "gst_set_waves", "gst_set_timing", "gst_kernel_times", "gst_eval_lnlike", "gst_sync",
            "gst_last_sweep_ms", "gst_debug_stamps")
 
 _P = ct.POINTER
@@ -111,6 +111,7 @@ def load(path: str | None = None):
     lib.gst_sync.argtypes = [ct.c_void_p, ct.c_void_p]
     lib.gst_set_path.argtypes = [ct.c_void_p, ct.c_int]
     lib.gst_get_path.argtypes = [ct.c_void_p, _P(ct.c_int)]
+    lib.gst_set_waves.argtypes = [ct.c_void_p, ct.c_int]
     lib.gst_set_timing.argtypes = [ct.c_void_p, ct.c_int]
     lib.gst_kernel_times.argtypes = [ct.c_void_p, _P(ct.c_double), _P(ct.c_int), ct.c_int]
     lib.gst_last_sweep_ms.argtypes = [ct.c_void_p, _P(ct.c_double)]

@@ -2,15 +2,17 @@
 from __future__ import annotations
 
 import os
+import re
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libgst.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("gst.hip", "gst_kernel.hpp", "gst_large.hpp",
-                                            "philox.hpp")]
+SOURCES = [os.path.join(CSRC, f) for f in ("gst.hip", "gst_inst.hip", "gst_shapes.h",
+                                            "gst_kernel.hpp", "gst_large.hpp", "philox.hpp")]
 HEADER = os.path.join(ROOT, "include", "gst.h")
 
 
@@ -31,19 +33,47 @@ def up_to_date():
 STAMPS_LIB = os.path.join(HERE, "libgst_stamps.so")
 
 
-def build(force: bool = False, verbose: bool = True, stamps: bool = False) -> str:
-    """Compile libgst.so (or the diagnostic libgst_stamps.so with per-stage cycle stamps)."""
+def shapes():
+    """The persistent kernel's shapes, from the GST_SHAPES list in csrc/gst_shapes.h."""
+    txt = open(os.path.join(CSRC, "gst_shapes.h")).read()
+    body = txt[txt.index("#define GST_SHAPES(X)"):txt.index("#define GST_PICK_NAME")]
+    return re.findall(r"X\((\d+), (\d+), (\d+), (\d+)\)", body)
+
+
+def build(force: bool = False, verbose: bool = True, stamps: bool = False,
+          jobs: int | None = None) -> str:
+    """Compile libgst.so (or the diagnostic libgst_stamps.so with per-stage cycle stamps):
+    gst.hip (ABI, large path) and one gst_inst.hip object per persistent-kernel shape,
+    compiled in parallel, linked into one shared library."""
     out = STAMPS_LIB if stamps else LIB
     if not force and not stamps and up_to_date():
         return LIB
+    objdir = os.path.join(HERE, "_obj_stamps" if stamps else "_obj")
+    os.makedirs(objdir, exist_ok=True)
     # -amdgpu-mfma-vgpr-form: keep the fp64 MFMA accumulators in VGPRs (gfx950's unified
     # register file); without it hipcc copies all 15 Gram tiles VGPR<->AGPR every k-step.
-    cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-mllvm", "-amdgpu-mfma-vgpr-form",
-           "-I", os.path.join(ROOT, "include"), "-I", CSRC,
-           os.path.join(CSRC, "gst.hip"), "-o", out + ".tmp"]
+    base = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
+            "-mllvm", "-amdgpu-mfma-vgpr-form",
+            "-I", os.path.join(ROOT, "include"), "-I", CSRC]
     if stamps:
-        cmd.insert(4, "-DGST_STAMPS")
+        base.append("-DGST_STAMPS")
+    units = [(os.path.join(CSRC, "gst.hip"), [], os.path.join(objdir, "gst.o"))]
+    for sh in shapes():
+        units.append((os.path.join(CSRC, "gst_inst.hip"), ["-DGST_SHAPE=" + ",".join(sh)],
+                      os.path.join(objdir, "inst_" + "_".join(sh) + ".o")))
+
+    def compile_one(u):
+        src, extra, obj = u
+        cmd = base + extra + ["-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        return obj
+
+    jobs = jobs or int(os.environ.get("MAX_JOBS", 0)) or min(8, os.cpu_count() or 1)
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(compile_one, units))
+    cmd = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

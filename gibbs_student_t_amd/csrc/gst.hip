@@ -14,6 +14,7 @@
 
 #include "gst.h"
 #include "gst_kernel.hpp"
+#include "gst_shapes.h"
 #include "gst_large.hpp"
 
 namespace {
@@ -44,6 +45,7 @@ struct Ctx {
   size_t tmfac_bytes = 0;
   int path_req = GST_PATH_AUTO;    // gst_set_path
   int path = GST_PATH_PERSISTENT;  // chosen by gst_model_set
+  int waves = GST_WAVES_AUTO;      // gst_set_waves
   std::vector<void*> allocs;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
@@ -90,39 +92,18 @@ void free_model(Ctx* cx) {
   free_tmfac(cx);
 }
 
-typedef void (*kfn_t)(const gst::DevModel*, const gst::DevState, const gst::DevRec,
-                      const gst::DevTape, int, int, long long, int, unsigned,
-                      unsigned long long, long long, int, double*, double*);
+using gst::kfn_t;
 
-template <int MT, int NS, int K0, int RA, bool TAPE, int WPB = 4, int OCC = 1>
-kfn_t kfn() {
-  return &gst::gst_sweep_kernel<MT, NS, K0, RA, TAPE, WPB, OCC>;
-}
-
-// Instantiated shapes: MT = padded matrix dim / 8, NS = TOA slots of 64, K0 = timing-model
-// panels of 8, RA = augmented-row index = 8*K0 + nfourier (the elimination length).
-// wpb: chains per workgroup (4, or 2 / 1 for sampling launches with fewer chains than
-// fill every SIMD; tape-mode parity launches always use 4).  occ2: the two-chains-per-SIMD
-// build (256 registers per lane), picked when the launch has more chains than SIMDs; with
-// at most one chain per SIMD the uncapped build keeps more of each chain in registers.
-kfn_t pick(int MT, int NS, int K0, int RA, bool tape, int wpb, bool occ2) {
-#define GST_CASE(mt, ns, k0, ra)                                                  \
-  if (MT == mt && NS == ns && K0 == k0 && RA == ra) {                             \
-    if (tape) return kfn<mt, ns, k0, ra, true>();                                 \
-    if (wpb == 1) return kfn<mt, ns, k0, ra, false, 1>();                         \
-    if (wpb == 2) return kfn<mt, ns, k0, ra, false, 2>();                         \
-    if (occ2 && gst::occ_for(mt, k0) == 2) return kfn<mt, ns, k0, ra, false, 4, 2>(); \
-    return kfn<mt, ns, k0, ra, false>();                                          \
-  }
-  GST_CASE(10, 2, 2, 76)   // J1713-like, n <= 128 (no_outlier datasets)
-  GST_CASE(10, 3, 2, 76)   // J1713+0747: n = 130, 30 red-noise components, 14 TM columns
-  GST_CASE(10, 4, 2, 76)   // n <= 256
-  GST_CASE(8, 2, 2, 56)    // <= 20 red-noise components, <= 16 TM columns
-  GST_CASE(8, 3, 2, 56)
-  GST_CASE(8, 4, 2, 56)
-  GST_CASE(10, 2, 3, 76)   // <= 26 components with 17..24 TM columns
-  GST_CASE(10, 3, 3, 76)
-  GST_CASE(10, 4, 3, 76)
+// The instance for a shape (gst_shapes.h; each shape's instances live in their own
+// translation unit, gst_inst.hip).  wpb: chains per workgroup (4, or 2 / 1 for sampling
+// launches with fewer chains than fill every SIMD; tape-mode parity launches always use 4).
+// occ2: the two-chains-per-SIMD build (256 registers per lane), picked when the launch has
+// more chains than SIMDs; with at most one chain per SIMD the uncapped build keeps more of
+// each chain in registers.  pair: two waves per chain (gst_set_waves).
+kfn_t pick(int MT, int NS, int K0, int RA, bool tape, int wpb, bool occ2, bool pair = false) {
+#define GST_CASE(mt, ns, k0, ra) \
+  if (MT == mt && NS == ns && K0 == k0 && RA == ra) return gst::GST_PICK_NAME(mt, ns, k0, ra)(tape, wpb, occ2, pair);
+  GST_SHAPES(GST_CASE)
 #undef GST_CASE
   return nullptr;
 }
@@ -597,18 +578,21 @@ static int launch(Ctx* cx, const gst_state* s, const gst_records* r, const gst_t
     if (wpb >= 1 && C <= cx->ncu) wpb = 1;
     else if (wpb >= 2 && C <= 2 * cx->ncu) wpb = 2;
   }
-  kfn_t k = pick(cx->MT, cx->NS, cx->K0, cx->raug, tape, wpb, C > 4 * cx->ncu);
+  // two waves per chain when every chain would otherwise leave a SIMD idle
+  const bool pair = !tape && !eval_only &&
+                    (cx->waves == GST_WAVES_TWO || (cx->waves == GST_WAVES_AUTO && C <= 2 * cx->ncu));
+  kfn_t k = pick(cx->MT, cx->NS, cx->K0, cx->raug, tape, wpb, C > 4 * cx->ncu, pair);
   if (!k) return fail("gst: no kernel instance");
-  // timing-model factor scratch: [C][slots with s < K0][64] doubles
+  // timing-model factor scratch: [C][waves per chain][slots with s < K0][64] doubles
   const int ntms = cx->MT * (cx->MT + 1) / 2 - (cx->MT - cx->K0) * (cx->MT - cx->K0 + 1) / 2;
-  const size_t need = (size_t)C * ntms * 64 * sizeof(double);
+  const size_t need = (size_t)C * (pair ? 2 : 1) * ntms * 64 * sizeof(double);
   if (need > cx->tmfac_bytes) {
     free_tmfac(cx);
     HIP_OK(hipMalloc(&cx->tmfac, need));
     cx->tmfac_bytes = need;
   }
   ds.tmfac = cx->tmfac;
-  const dim3 grid((C + wpb - 1) / wpb), block(64 * wpb);
+  const dim3 grid(pair ? C : (C + wpb - 1) / wpb), block(pair ? 128 : 64 * wpb);
   hipStream_t st = (hipStream_t)stream;
   HIP_OK(hipEventRecord(cx->ev0, st));
   hipLaunchKernelGGL(k, grid, block, 0, st, cx->dmd, ds, dr, dt, C, nsweeps, sweep0,
@@ -662,6 +646,14 @@ int gst_set_path(void* ctx, int path) {
   if (!cx) return fail("gst_set_path: null ctx");
   if (path < GST_PATH_AUTO || path > GST_PATH_LARGE) return fail("gst_set_path: bad path");
   cx->path_req = path;
+  return 0;
+}
+
+int gst_set_waves(void* ctx, int waves) {
+  Ctx* cx = static_cast<Ctx*>(ctx);
+  if (!cx) return fail("gst_set_waves: null ctx");
+  if (waves < GST_WAVES_AUTO || waves > GST_WAVES_TWO) return fail("gst_set_waves: bad value");
+  cx->waves = waves;
   return 0;
 }
 

@@ -3,7 +3,8 @@
 // One 64-lane wavefront owns one chain for a whole launch of `nsweeps` sweeps of the
 // reference sampler (/root/reference/gibbs.py, Gibbs.sample loop gibbs.py:354-380).
 // Chains are independent, so waves never synchronise with each other: there is no
-// __syncthreads, only in-order same-wave LDS traffic.
+// __syncthreads, only in-order same-wave LDS traffic (except in the two-waves-per-chain
+// build, PAIR below, whose two waves exchange MH likelihoods once per round).
 //
 // Matrix layout ("8x8 cyclic"): lane = 8p + q owns elements (8r+p, 8s+q) of the symmetric
 // system matrix, r >= s, in registers L[SL(r,s)].  Internal column order is
@@ -89,7 +90,7 @@ struct DevModel {
   double tm_phiinv, logdet_phi_tm;
   double sum_lfreq, sum_ldf;  // sum_k log f_k, sum_k log df_k (closed-form log|phi|)
   double log_fyr, log_12pi2;
-  unsigned long long* stamps;  // diagnostic build only (GST_STAMPS): [C][8] cycle sums
+  unsigned long long* stamps;  // diagnostic build only (GST_STAMPS): [C][GST_NSTAMP]
 };
 
 struct DevState {
@@ -117,10 +118,13 @@ constexpr int TP_WHITE = 0, TP_HYPER = 80, TP_DELTA = 120;
 // loads; the 8 owner lanes (q == column residue) write it.  Row stride MT = 10 doubles puts
 // the 8 p-rows of a 128-bit read in distinct bank groups (80 B apart).
 
+// diagnostic builds: slots 0-15 cycle sums (tools/stage_profile.py), 16-19 event counts
+constexpr int GST_NSTAMP = 20;
 #ifdef GST_STAMPS
 #define GST_STAMP_DECL \
-  unsigned long long st_acc[16] = {0}, st_t0 = 0, st_s0 = 0;
+  unsigned long long st_acc[GST_NSTAMP] = {0}, st_t0 = 0, st_s0 = 0;
 #define GST_SUB_BEGIN st_s0 = __builtin_amdgcn_s_memtime();
+#define GST_COUNT(i) st_acc[i] += 1;
 #define GST_SUB_END(i)                                            \
   {                                                               \
     const unsigned long long t1_ = __builtin_amdgcn_s_memtime(); \
@@ -136,9 +140,10 @@ constexpr int TP_WHITE = 0, TP_HYPER = 80, TP_DELTA = 120;
   }
 #define GST_STAMP_FLUSH                                             \
   if (md.stamps && lane == 0)                                       \
-    for (int i_ = 0; i_ < 16; ++i_) md.stamps[(size_t)c * 16 + i_] += st_acc[i_];
+    for (int i_ = 0; i_ < GST_NSTAMP; ++i_) md.stamps[(size_t)c * GST_NSTAMP + i_] += st_acc[i_];
 #else
 #define GST_SUB_BEGIN
+#define GST_COUNT(i)
 #define GST_SUB_END(i)
 #define GST_STAMP_DECL
 #define GST_STAMP_START
@@ -634,12 +639,19 @@ __device__ __forceinline__ void chol_stats(CholCtx& cc) {
 // per SIMD the kernel is compiled for: 2 caps it at 256 registers per lane (VGPR + AGPR)
 // so that two workgroups share a CU and each SIMD interleaves two chains' dependency
 // chains (the kernel is latency-bound per wave).
-template <int MT, int NS, int K0, int RA, bool TAPE, int WPB = 4, int OCC = 1>
+// PAIR (with WPB = 2): the two waves of a workgroup run ONE chain, for launches with at most
+// one chain per two SIMDs (config 3's 512 chains).  Both waves run every stage on identical
+// state and variates; in the hyper block they evaluate different MH points per round -- the
+// next proposal, and the one after it on the branch the chain's acceptance history predicts
+// -- and exchange the lnL values through LDS, so that a round settles one or two MH steps
+// (DESIGN.md section 8).
+template <int MT, int NS, int K0, int RA, bool TAPE, int WPB = 4, int OCC = 1, bool PAIR = false>
 __global__ void __launch_bounds__(64 * WPB, OCC)
     gst_sweep_kernel(const DevModel* __restrict__ mds, const DevState st, const DevRec rec, const DevTape tape,
                      int C, int nsweeps, long long sweep0, int record_every, unsigned mask,
                      unsigned long long seed, long long chain0, int eval_only, double* out_w,
                      double* out_h) {
+  static_assert(!PAIR || (WPB == 2 && !TAPE), "pair mode: one chain per 2-wave workgroup");
   constexpr int NSL = SL(MT, 0);
   constexpr int NT = MT / 2;          // 16-wide MFMA tiles
   constexpr int NTT = NT * (NT + 1) / 2;
@@ -649,10 +661,13 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   constexpr int S0RD = s0r_doubles(MT, K0);
   static_assert(s0r_need(MT, NS) <= S0RD, "S0 region too small for the stage scratch");
   __shared__ double smem[WPB][lds_doubles(MT, K0)];
+  __shared__ double xchg[PAIR ? 2 : 1][2][2];  // pair mode: [round parity][wave] {lnL, failed}
+  __shared__ int xdrew[PAIR ? 1 : 1];          // pair mode: the b draw happened this sweep
 
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int c = blockIdx.x * WPB + wv;
+  const int c = PAIR ? (int)blockIdx.x : (int)blockIdx.x * WPB + wv;
+  const int role = PAIR ? wv : 0;   // pair mode: which of the chain's two waves
   if (c >= C) return;
   // the chain's dataset (run_sims grids batch many datasets x models per launch): every
   // field of md is wave-uniform, so it is read with scalar loads
@@ -686,7 +701,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   // the TM factor slots (s < K0) wait in global scratch while the hyper block runs
   // per-chain rows of the state arrays: wave-uniform base pointers (SGPRs), so every
   // per-lane access is base + 32-bit lane offset
-  double* const tmf = st.tmfac + (size_t)c * NTMS * 64;
+  double* const tmf = st.tmfac + ((size_t)c * (PAIR ? 2 : 1) + role) * NTMS * 64;
   double* const xrow = st.x + (size_t)c * md.P;
   double* const brow = st.b + (size_t)c * md.m;
   double* const zrow = st.z + (size_t)c * nst;
@@ -1015,6 +1030,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
 
   // b-marginalised likelihood at xq (gibbs.py:288-329); factor left in L.
   auto lnl_hyper = [&](const double (&xq)[4], int& failed) __attribute__((always_inline)) -> double {
+    GST_COUNT(16)
     GST_SUB_BEGIN
     const double lA = pget(xq, md.idx_logA);
     const double g = pget(xq, md.idx_gamma);
@@ -1060,7 +1076,8 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     return ll;
   };
 
-  const bool rec_on = record_every > 0 && !eval_only;
+  const bool rec_on = record_every > 0 && !eval_only && role == 0;
+  int hacc = 0, hrej = 0;   // pair mode: hyper-MH acceptance history (branch prediction)
   GST_STAMP_START
   compute_Tb();
   if (eval_only) nsweeps = 1;
@@ -1076,8 +1093,10 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       if (ri < rec.nrec) {
         const size_t base = (size_t)c * rec.nrec + ri;
         if (rec.x && lane < P) rec.x[base * P + lane] = pget(xv, lane);
+        // from the state row, not bsc: bsc shares S0R with S0 and is stale after a sweep
+        // that skipped the b draw (gibbs.py:373)
         if (rec.b)
-          for (int j = lane; j < m; j += 64) rec.b[base * m + j] = bsc[j];
+          for (int j = lane; j < m; j += 64) rec.b[base * m + j] = brow[j];
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
           const int t = 64 * s + lane;
@@ -1232,7 +1251,147 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     // x for the b draw when the factor left in registers belongs to a rejected proposal.
     bool redraw = false;
     int fb = 0;
-    if ((mask & 6u) || eval_only) {
+    int owner = 0;   // the wave whose registers hold the factor at the final x (pair mode)
+    if constexpr (PAIR) {
+      if (mask & 6u) {
+        gram_and_tm(xv);   // both waves: identical S0 in each wave's own LDS region
+        if (fail_tm) status |= 1;
+        GST_STAMP(2)
+        double l0 = 0.0, p0 = 0.0;
+        owner = -1;
+        bool init = (mask & 2u) != 0;
+        int j = init ? 0 : NHYPER, rp = 0;
+        // first step >= s whose proposal from xb is inside the prior (the others are
+        // rejected without a likelihood, gibbs.py:100-104 with lnprior = -inf)
+        auto next_in = [&](const double (&xb)[4], int s) __attribute__((always_inline)) -> int {
+          for (; s < NHYPER; ++s) {
+            double qv[4], E;
+            int par;
+            (void)propose(xb, qv, NWHITE + s, E, par);
+            if (lnprior(qv) != -INFINITY) break;
+          }
+          return s;
+        };
+        // one sequential MH step (gibbs.py:99-110) at step s with the lnL of its point
+        auto decide = [&](int s, double l1, bool f1, int who) __attribute__((always_inline)) {
+          if (f1) status |= 1;
+          double qv[4], E;
+          int par;
+          const double luacc = propose(xv, qv, NWHITE + s, E, par);
+          const double p1 = lnprior(qv);
+          if ((l1 + p1) - (l0 + p0) > luacc) {
+            GST_COUNT(18)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) xv[t] = qv[t];
+            l0 = l1;
+            p0 = p1;
+            owner = who;
+            ++hacc;
+            return true;
+          }
+          owner = -1;
+          ++hrej;
+          return false;
+        };
+        // Each round wave 0 evaluates the next point the sequential sampler needs (the
+        // initial x, then the next in-prior proposal sa) and wave 1 a speculative one: the
+        // step after sa on the branch (accept / reject) the chain's acceptance history
+        // predicts, else on the other branch, else -- no proposal left -- the current x
+        // (the reject branch's final state, for the b draw).  A last round refactors the
+        // final x when no wave holds its factor and the b draw needs it.
+#pragma unroll 1
+        while (true) {
+          const int sa = init ? -1 : next_in(xv, j);
+          bool fin = false;
+          if (sa >= NHYPER) {
+            if (!(mask & 4u)) break;
+            redraw = true;
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+              if (t < P) redraw = redraw && (xv[t] != x_last0);      // gibbs.py:373
+            if (mask & 128u) redraw = true;
+            if (!redraw || owner >= 0) break;
+            fin = true;
+          }
+          double qa[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) qa[t] = xv[t];
+          int kind = 0, sb = NHYPER;   // wave 1: 0 idle, 1 accept branch, 2 reject branch, 3 x
+          if (!fin) {
+            if (!init) {
+              double E;
+              int par;
+              (void)propose(xv, qa, NWHITE + sa, E, par);
+            }
+            const int sbR = next_in(xv, sa + 1);
+            const int sbA = init ? NHYPER : next_in(qa, sa + 1);
+            if (!init && hacc >= hrej && sbA < NHYPER) {
+              kind = 1;
+              sb = sbA;
+            } else if (sbR < NHYPER) {
+              kind = 2;
+              sb = sbR;
+            } else if (!init && (mask & 4u) && owner != 1) {
+              kind = 3;
+            }
+          }
+          double xq[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) xq[t] = role == 0 ? qa[t] : xv[t];
+          if (role == 1 && (kind == 1 || kind == 2)) {
+            double E;
+            int par;
+            (void)propose(kind == 1 ? qa : xv, xq, NWHITE + sb, E, par);
+          }
+          GST_COUNT(17)
+          double lm = 0.0;
+          int fm = 0;
+          if (role == 0 || kind != 0) lm = lnl_hyper(xq, fm);
+          if (lane == 0) {
+            xchg[rp][role][0] = lm;
+            xchg[rp][role][1] = (double)fm;
+          }
+          __syncthreads();
+          const double lA = xchg[rp][0][0], lB = xchg[rp][1][0];
+          const bool fA = xchg[rp][0][1] != 0.0, fB = xchg[rp][1][1] != 0.0;
+          rp ^= 1;   // the next round writes the other buffer: no second barrier needed
+          if (fin) {
+            fb = fA;
+            owner = 0;
+            break;
+          }
+          const int prev = owner;
+          if (init) {
+            if (fA) status |= 1;
+            l0 = lA;
+            p0 = lnprior(xv);
+            owner = fA ? -1 : 0;
+            init = false;
+            j = NHYPER;
+            if (kind == 2) {
+              decide(sb, lB, fB, 1);
+              j = sb + 1;
+            }
+          } else if (decide(sa, lA, fA, 0)) {
+            j = sa + 1;
+            if (kind == 1) {
+              decide(sb, lB, fB, 1);
+              j = sb + 1;
+            }
+          } else {
+            j = sa + 1;
+            if (kind == 2) {
+              decide(sb, lB, fB, 1);
+              j = sb + 1;
+            } else if (kind == 3) {
+              owner = fB ? -1 : 1;
+            } else if (kind == 0 && prev == 1) {
+              owner = 1;   // wave 1 sat out: its factor of x is intact
+            }
+          }
+        }
+      }
+    } else if ((mask & 6u) || eval_only) {
       gram_and_tm(xv);
       if (fail_tm) status |= 1;
       GST_STAMP(2)
@@ -1281,6 +1440,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
           continue;
         }
         if ((l1 + p1) - (l0 + p0) > luacc) {
+          GST_COUNT(18)
 #pragma unroll
           for (int j = 0; j < 4; ++j) xv[j] = qv[j];
           l0 = l1;
@@ -1294,10 +1454,12 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     if (eval_only) return;
     GST_STAMP(3)
 
-    if (redraw) {
+    bool drew = false;
+    if (redraw && role == owner) {
       if (fb) {
         status |= 2;
       } else {
+        drew = true;
         GST_SUB_BEGIN
 #pragma unroll
         for (int s = 0; s < K0; ++s)
@@ -1401,6 +1563,20 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         lds_order();
         compute_Tb();
         GST_SUB_END(14)
+      }
+    }
+    if constexpr (PAIR) {
+      // hand the new b to the other wave: its copy of bsc, then its own y = r - T b
+      if (mask & 6u) {
+        if (drew) {
+          double* pb = smem[role ^ 1] + (bsc - smem[role]);
+          for (int j = lane; j < m; j += 64) pb[j] = bsc[j];
+        }
+        if (role == (owner >= 0 ? owner : 0) && lane == 0) xdrew[0] = drew ? 1 : 0;
+        __syncthreads();
+        const bool got = xdrew[0] != 0;
+        __syncthreads();   // xdrew is rewritten next sweep
+        if (got && role != owner) compute_Tb();
       }
     }
 
@@ -1542,6 +1718,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   }
 
   GST_STAMP(6)
+  if (role != 0) return;   // pair mode: wave 0 writes the chain's state
   GST_STAMP_FLUSH
   // ---------------- write back ----------------
   if (lane < P) xrow[lane] = pget(xv, lane);

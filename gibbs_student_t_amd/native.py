@@ -132,6 +132,12 @@ class NativeSampler:
         self.state = None
         self.dataset = None
 
+    def set_waves(self, waves="auto"):
+        """Waves per chain of the persistent path's sampling launches (gst_set_waves):
+        "auto" (two when C <= 2 x CUs), 1 or 2.  The draws are bitwise the same."""
+        code = {"auto": 0, 1: 1, 2: 2}[waves]
+        _abi.check(self.lib, self.lib.gst_set_waves(self.ctx, code), "gst_set_waves")
+
     # ---- state ---------------------------------------------------------------------
     def alloc(self, C: int, dataset=None):
         """Allocate C chains; ``dataset[c]`` is chain c's dataset index (default all 0)."""

@@ -182,6 +182,15 @@ enum gst_path { GST_PATH_AUTO = 0, GST_PATH_PERSISTENT = 1, GST_PATH_LARGE = 2 }
 int gst_set_path(void* ctx, int path);
 int gst_get_path(void* ctx, int* path);
 
+/* Waves per chain on the persistent path.  A sampling launch with at most one chain per two
+ * SIMDs (C <= 2 x CUs, e.g. BASELINE config 3's 512 chains) runs each chain on two waves
+ * that split the red-noise MH block's likelihood evaluations (AUTO, the default); the
+ * chain's draws are bitwise those of the one-wave kernel.  GST_WAVES_ONE / GST_WAVES_TWO
+ * force either kernel for every sampling launch (tape-mode and gst_eval_lnlike launches
+ * always run one wave per chain). */
+enum gst_waves { GST_WAVES_AUTO = 0, GST_WAVES_ONE = 1, GST_WAVES_TWO = 2 };
+int gst_set_waves(void* ctx, int waves);
+
 /* Per-kernel timing of the large path (HIP events around every launch of the next
  * gst_sweep / gst_eval_lnlike calls while enabled).  gst_kernel_times fills ms[k] (summed
  * milliseconds) and launches[k] for kernel kinds k < nkinds (enum gst_kernel_kind). */
@@ -192,8 +201,10 @@ enum gst_kernel_kind {
 int gst_set_timing(void* ctx, int on);
 int gst_kernel_times(void* ctx, double* ms, int* launches, int nkinds);
 
-/* Diagnostic builds (-DGST_STAMPS) only: per-chain per-stage s_memtime cycle sums are
- * accumulated into dev_buf[C][8]; returns an error in production builds. */
+/* Diagnostic builds (-DGST_STAMPS) only: per-chain per-stage s_memtime cycle sums (slots
+ * 0-15) and event counts (16: red-noise likelihoods, 17: two-wave rounds, 18: accepted
+ * red-noise proposals) are accumulated into dev_buf[C][20]; returns an error in production
+ * builds. */
 int gst_debug_stamps(void* ctx, unsigned long long* dev_buf);
 
 /* Kernel-level timing of the last gst_sweep on its stream (hipEvents), milliseconds. */

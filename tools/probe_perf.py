@@ -1,4 +1,5 @@
-"""Quick GPU timing probe: sweeps/s of the sweep kernel at several chain counts."""
+"""Quick GPU timing probe: sweeps/s of the sweep kernel at several chain counts (and
+waves per chain)."""
 import sys
 import time
 
@@ -15,8 +16,12 @@ def main():
     psr = data.j1713()
     pta = PTA(psr)
     cfg = dict(model="mixture", vary_df=True, theta_prior="beta")
-    for C in [int(a) for a in (sys.argv[1:] or ["256", "1024", "2048"])]:
+    # arguments: C or C:waves (waves per chain: 1, 2; default auto)
+    for arg in (sys.argv[1:] or ["256", "1024", "2048"]):
+        C, _, w = arg.partition(":")
+        C = int(C)
         ns = NativeSampler(pta, cfg, 0)
+        ns.set_waves(int(w) if w else "auto")
         ns.alloc(C)
         rng = np.random.default_rng(0)
         x0 = np.stack([[rng.uniform(1, 7), rng.uniform(-18, -12), rng.uniform(-10, -5)]
@@ -33,7 +38,7 @@ def main():
         dt = time.perf_counter() - t0
         kms = ns.last_kernel_ms()
         st = ns.get_state()
-        print(f"C={C} sweeps={S} wall={dt*1e3:.1f} ms kernel={kms:.1f} ms  "
+        print(f"C={C} waves={w or 'auto'} sweeps={S} wall={dt*1e3:.1f} ms kernel={kms:.1f} ms  "
               f"-> {C*S/dt:.3e} chain-sweeps/s, {dt/S*1e6:.1f} us/sweep; "
               f"status!=0: {(st['status']!=0).sum()}", flush=True)
         ns.close()
