@@ -25,7 +25,7 @@ ABI_VERSION = 2
 EXPORTS = ("gst_version", "gst_tape_stride", "gst_last_error", "gst_ctx_create",
            "gst_ctx_destroy", "gst_model_set", "gst_model_set_batch", "gst_model_info",
            "gst_sweep", "gst_set_path", "gst_get_path", "gst_set_waves", "gst_set_timing", "gst_kernel_times", "gst_eval_lnlike", "gst_sync",
-           "gst_last_sweep_ms", "gst_debug_stamps")
+           "gst_last_sweep_ms", "gst_debug_stamps", "gst_simulate")
 
 _P = ct.POINTER
 _D = _P(ct.c_double)
@@ -67,6 +67,19 @@ class Records(ct.Structure):
 
 class Tape(ct.Structure):
     _fields_ = [("data", ct.c_void_p), ("stride", ct.c_int)]
+
+
+class SimDesc(ct.Structure):
+    """gst_sim_desc (device pointers)."""
+    _fields_ = [("n", ct.c_int), ("nfourier", ct.c_int), ("ntm", ct.c_int),
+                ("ndatasets", ct.c_int),
+                ("F", ct.c_void_p), ("log_f", ct.c_void_p), ("log_df", ct.c_void_p),
+                ("log_fyr", ct.c_double), ("U", ct.c_void_p), ("red", ct.c_void_p),
+                ("toaerrs", ct.c_void_p), ("theta", ct.c_void_p), ("sigma_out", ct.c_void_p),
+                ("log10_A", ct.c_void_p), ("gamma", ct.c_void_p), ("dof", ct.c_void_p),
+                ("seed", ct.c_ulonglong), ("dataset0", ct.c_longlong),
+                ("residuals", ct.c_void_p), ("toaerrs_out", ct.c_void_p), ("z", ct.c_void_p),
+                ("residuals_clean", ct.c_void_p)]
 
 
 _lib = None
@@ -116,6 +129,7 @@ def load(path: str | None = None):
     lib.gst_kernel_times.argtypes = [ct.c_void_p, _P(ct.c_double), _P(ct.c_int), ct.c_int]
     lib.gst_last_sweep_ms.argtypes = [ct.c_void_p, _P(ct.c_double)]
     lib.gst_debug_stamps.argtypes = [ct.c_void_p, ct.c_void_p]
+    lib.gst_simulate.argtypes = [_P(SimDesc), ct.c_void_p]
     for name in EXPORTS:
         if name != "gst_version":
             getattr(lib, name).restype = ct.c_int

@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libgst.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("gst.hip", "gst_inst.hip", "gst_shapes.h",
+SOURCES = [os.path.join(CSRC, f) for f in ("gst.hip", "gst_inst.hip", "gst_shapes.h", "gst_sim.hpp",
                                             "gst_kernel.hpp", "gst_large.hpp", "philox.hpp")]
 HEADER = os.path.join(ROOT, "include", "gst.h")
 

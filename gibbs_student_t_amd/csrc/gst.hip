@@ -16,6 +16,7 @@
 #include "gst_kernel.hpp"
 #include "gst_shapes.h"
 #include "gst_large.hpp"
+#include "gst_sim.hpp"
 
 namespace {
 
@@ -688,6 +689,51 @@ int gst_kernel_times(void* ctx, double* ms, int* launches, int nkinds) {
     ms[k] += f;
     launches[k] += 1;
   }
+  return 0;
+}
+
+int gst_simulate(const gst_sim_desc* d, void* stream) {
+  if (!d) return fail("gst_simulate: null descriptor");
+  if (d->n <= 0 || d->ndatasets < 0 || d->ntm < 0 || d->nfourier < 0)
+    return fail("gst_simulate: bad sizes");
+  if (d->ndatasets == 0) return 0;
+  if (d->nfourier > gst::SIM_MAX_NF || d->ntm > gst::SIM_MAX_NF)
+    return fail("gst_simulate: nfourier and ntm must be <= 512");
+  if (d->residuals_clean && d->ntm > gst::SIM_MAX_TM_CLEAN)
+    return fail("gst_simulate: the clean twin needs ntm <= 64");
+  if (!d->red && (!d->F || !d->log_f || !d->log_df) && d->nfourier > 0)
+    return fail("gst_simulate: power-law red noise needs F, log_f and log_df");
+  if ((d->ntm > 0 && !d->U) || !d->theta || !d->sigma_out || !d->dof ||
+      (!d->red && (!d->log10_A || !d->gamma)) || !d->residuals || !d->toaerrs_out || !d->z)
+    return fail("gst_simulate: missing pointer");
+  gst::SimArgs a{};
+  a.n = d->n;
+  a.nf = d->red ? 0 : d->nfourier;
+  a.ntm = d->ntm;
+  a.D = d->ndatasets;
+  a.F = d->F;
+  a.lf = d->log_f;
+  a.ldf = d->log_df;
+  a.log_fyr = d->log_fyr;
+  a.log_12pi2 = std::log(12.0) + 2.0 * std::log(M_PI);
+  a.U = d->U;
+  a.red = d->red;
+  a.err_in = d->toaerrs;
+  a.theta = d->theta;
+  a.sigma_out = d->sigma_out;
+  a.log10_A = d->log10_A;
+  a.gamma = d->gamma;
+  a.dof = d->dof;
+  a.k0 = (uint32_t)(d->seed & 0xffffffffull);
+  a.k1 = (uint32_t)(d->seed >> 32);
+  a.ds0 = d->dataset0;
+  a.r = d->residuals;
+  a.err = d->toaerrs_out;
+  a.z = d->z;
+  a.r_clean = d->residuals_clean;
+  hipLaunchKernelGGL(gst::gst_simulate_kernel, dim3(d->ndatasets), dim3(gst::SIM_BLOCK), 0,
+                     (hipStream_t)stream, a);
+  HIP_OK(hipGetLastError());
   return 0;
 }
 

@@ -66,12 +66,20 @@ class Entry:
 
 def build_grid(thetas=(0.05, 0.1, 0.15), realisations=1, models=tuple(MODELS),
                seed=2017, sigma_out=1e-6, red_source="powerlaw", dofs=(None,),
-               kinds=("outlier", "no_outlier")):
+               kinds=("outlier", "no_outlier"), generator="host", device=0):
     """The study's entries in a fixed global order (realisation-major).
 
-    Realisation k at outlier fraction theta and white-noise dof uses simulate_data with a
-    seed derived from (seed, k, theta, dof), so entry lists built on different ranks agree.
+    ``generator="host"``: realisation k at outlier fraction theta and white-noise dof uses
+    data.simulate_data with a seed derived from (seed, k, theta, dof).  ``"device"``: every
+    (k, theta, dof) dataset of the grid is drawn in ONE gst_simulate launch (simulate.py),
+    dataset id = its position in that order.  Either way entry lists built on different
+    ranks agree.
     """
+    if generator == "device":
+        return _grid_on_device(thetas, realisations, models, seed, sigma_out, red_source,
+                               dofs, kinds, device)
+    if generator != "host":
+        raise ValueError("generator must be 'host' or 'device'")
     entries = []
     for k in range(realisations):
         for ti, theta in enumerate(thetas):
@@ -85,6 +93,32 @@ def build_grid(thetas=(0.05, 0.1, 0.15), realisations=1, models=tuple(MODELS),
                     for mdl in models:
                         entries.append(Entry(kind, float(theta), sd, mdl, pta, dof,
                                              {"z_true": out.meta["z_true"]}))
+    return entries
+
+
+def _grid_on_device(thetas, realisations, models, seed, sigma_out, red_source, dofs, kinds,
+                    device):
+    from . import simulate
+    raw = gdata.load_j1713_raw()
+    mjd = raw["mjd_int"].astype(np.float64) + raw["mjd_frac"]
+    toas = mjd * gdata.DAY_SEC
+    M = gdata.design_matrix(mjd, raw["par"], raw["fit"])
+    combos = [(k, float(theta), dof) for k in range(realisations) for theta in thetas
+              for dof in dofs]
+    red = raw["red"] * gdata.DAY_SEC if red_source == "red.txt" else None
+    sim = simulate.simulate_batch(
+        toas, M, len(combos), seed=seed, theta=[c[1] for c in combos], sigma_out=sigma_out,
+        dof=[0.0 if c[2] is None else float(c[2]) for c in combos], red=red,
+        clean="no_outlier" in kinds, device=device)
+    prs = simulate.pairs(toas, M, sim, name="J1713+0747", freqs=raw["freq_mhz"])
+    entries = []
+    for i, ((k, theta, dof), (out, clean)) in enumerate(zip(combos, prs)):
+        pair = {"outlier": out, "no_outlier": clean}
+        for kind in kinds:
+            pta = PTA(pair[kind])
+            for mdl in models:
+                entries.append(Entry(kind, theta, i, mdl, pta, dof,
+                                     {"z_true": out.meta["z_true"], "generator": "device"}))
     return entries
 
 
@@ -257,12 +291,17 @@ def main(argv=None):
     ap.add_argument("--record-every", type=int, default=1)
     ap.add_argument("--outdir", default=None)
     ap.add_argument("--seed", type=int, default=2017)
+    ap.add_argument("--generator", choices=("device", "host"), default="device",
+                    help="draw the grid's datasets in one GPU launch (default) or per "
+                         "dataset with NumPy")
+    ap.add_argument("--red-source", choices=("powerlaw", "red.txt"), default="powerlaw")
     args = ap.parse_args(argv)
     from . import dist
     rank, local, world = dist.init()
     dofs = tuple([None] + list(args.dofs)) if args.dofs else (None,)
     entries = build_grid(args.thetas, args.realisations, tuple(args.models), args.seed,
-                         dofs=dofs)
+                         red_source=args.red_source, dofs=dofs, generator=args.generator,
+                         device=local)
     per = (len(entries) + world - 1) // world
     mine = entries[rank * per:(rank + 1) * per]
     if not mine:

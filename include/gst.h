@@ -210,6 +210,44 @@ int gst_debug_stamps(void* ctx, unsigned long long* dev_buf);
 /* Kernel-level timing of the last gst_sweep on its stream (hipEvents), milliseconds. */
 int gst_last_sweep_ms(void* ctx, double* ms);
 
+/* Batched synthetic pulsars on the current device: the simulate_data.py:10-39 recipe for
+ * `ndatasets` datasets in one launch (one workgroup per dataset), Philox variates keyed by
+ * (seed, dataset0 + d).  Replaces simulate_data() + the par/tim round trip through
+ * libstempo (simulate_data.py:12-37, run_sims.py:41-51).  All pointers are DEVICE pointers;
+ * per-dataset outputs are [ndatasets][n].
+ *   error bars   toaerrs[n] if given, else 10^(-7 + 0.2 N(0,1)) s         (:15)
+ *   red noise    red[n] if given (e.g. red.txt), else F (sqrt(phi) N(0,1)) with the power
+ *                law phi_k = A^2/(12 pi^2) fyr^(gamma-3) f_k^-gamma df_k        (:21)
+ *   outliers     z_t ~ Bernoulli(theta)                                   (:24)
+ *   residuals    red + ((1 - z) err + z sigma_out) xi, xi ~ N(0,1) or Student-t(dof) for
+ *                dof > 0, then the timing model refit out: r - U (U^T r)  (:26)
+ *   clean twin   (residuals_clean may be NULL) the no_outlier dataset (:35-37): outlier
+ *                TOAs deleted (their entries set to 0) and the timing model refit on the
+ *                kept TOAs (needs ntm <= 64).
+ * Limits: nfourier <= 512, ntm <= 512. */
+typedef struct gst_sim_desc {
+  int n, nfourier, ntm, ndatasets;
+  const double* F;        /* [n][nfourier] Fourier basis (may be NULL when red is given) */
+  const double* log_f;    /* [nfourier] log f_k (Hz) */
+  const double* log_df;   /* [nfourier] log df_k */
+  double log_fyr;         /* log(1 / yr in Hz) */
+  const double* U;        /* [n][ntm] orthonormal timing-model basis (SVD of M) */
+  const double* red;      /* [n] fixed red-noise realisation (s) or NULL */
+  const double* toaerrs;  /* [n] fixed error bars (s) or NULL */
+  const double* theta;    /* [ndatasets] outlier fraction */
+  const double* sigma_out;/* [ndatasets] outlier scatter (s) */
+  const double* log10_A;  /* [ndatasets] red-noise amplitude (power-law draw) */
+  const double* gamma;    /* [ndatasets] red-noise spectral index */
+  const double* dof;      /* [ndatasets] Student-t dof of the white noise, <= 0: Gaussian */
+  unsigned long long seed;
+  long long dataset0;     /* global index of dataset 0 (shards give the same datasets) */
+  double* residuals;      /* out [ndatasets][n] */
+  double* toaerrs_out;    /* out [ndatasets][n] */
+  double* z;              /* out [ndatasets][n] injected outlier flags (0 / 1) */
+  double* residuals_clean;/* out [ndatasets][n] or NULL */
+} gst_sim_desc;
+int gst_simulate(const gst_sim_desc* desc, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

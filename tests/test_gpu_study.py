@@ -14,8 +14,9 @@ from gibbs_student_t_amd import run_sims  # noqa: E402
 from gibbs_student_t_amd.native import NativeSampler  # noqa: E402
 
 
-def test_study_writes_reference_layout(tmp_path):
-    entries = run_sims.build_grid(thetas=(0.05, 0.15), realisations=1)
+@pytest.mark.parametrize("generator", ["host", "device"])
+def test_study_writes_reference_layout(tmp_path, generator):
+    entries = run_sims.build_grid(thetas=(0.05, 0.15), realisations=1, generator=generator)
     st = run_sims.Study(entries, chains=1, seed=3)
     _, secs = st.run(260, burn=100, outdir=str(tmp_path), chunk=64)
     st.close()
@@ -57,9 +58,12 @@ def test_study_chain_equals_standalone_sampler():
     ns.close()
 
 
-def test_outlier_model_finds_injected_outliers():
-    """Mixture model on an outlier dataset: true outliers get the high outlier probability."""
-    entries = [e for e in run_sims.build_grid(thetas=(0.15,), realisations=1, models=("beta",))
+@pytest.mark.parametrize("generator", ["host", "device"])
+def test_outlier_model_finds_injected_outliers(generator):
+    """Mixture model on an outlier dataset: true outliers get the high outlier probability
+    (with the datasets drawn per dataset on the host or all at once on the GPU)."""
+    entries = [e for e in run_sims.build_grid(thetas=(0.15,), realisations=1, models=("beta",),
+                                              generator=generator)
                if e.kind == "outlier"]
     st = run_sims.Study(entries, chains=64, seed=5)
     recs, _ = st.run(600, burn=200, chunk=200, keys=("x", "pout"))
