@@ -118,7 +118,7 @@ constexpr int TP_WHITE = 0, TP_HYPER = 80, TP_DELTA = 120;
 // loads; the 8 owner lanes (q == column residue) write it.  Row stride MT = 10 doubles puts
 // the 8 p-rows of a 128-bit read in distinct bank groups (80 B apart).
 
-// diagnostic builds: slots 0-15 cycle sums (tools/stage_profile.py), 16-19 event counts
+// diagnostic builds: slots 0-15 and 19 cycle sums (tools/stage_profile.py), 16-18 event counts
 constexpr int GST_NSTAMP = 20;
 #ifdef GST_STAMPS
 #define GST_STAMP_DECL \
@@ -1058,9 +1058,10 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     CholCtx cc{colq, phbuf, lane, p, q, raug, 1.0, 0.0, 0, 0, {tm_apr, 1.0}, {tm_zr, 0.0}};
     GST_SUB_END(7)
     chol_range<MT, K0, RA>(L, cc);
+    GST_SUB_END(8)
     chol_harvest<MT, 8 * K0, RA, RA>(L, cc);
     chol_stats<8 * K0, RA>(cc);
-    GST_SUB_END(8)
+    GST_SUB_END(19)
     f_apr[0] = cc.apr[0];
     f_apr[1] = cc.apr[1];
     f_zr[0] = cc.zr[0];

@@ -16,7 +16,7 @@ from gibbs_student_t_amd.model import PTA  # noqa: E402
 from gibbs_student_t_amd.native import NativeSampler  # noqa: E402
 
 STAGES = ["record", "white MH", "Gram+TM elim", "hyper MH (11 chol)", "b draw",
-          "theta+z+alpha", "nu", "(hyper: phi + S0 load)", "(hyper: F chol)",
+          "theta+z+alpha", "nu", "(hyper: phi + S0 load)", "(hyper: F elimination)",
           "(gram: MFMA loop)", "(gram: transpose+prior)", "(gram: TM chol)",
           "(b: yinv + rhs)", "(b: back-subst)", "(b: T b)", "(white: lnL evals)"]
 
@@ -48,6 +48,8 @@ def main():
     for i, nm in enumerate(STAGES):
         print(f"  {nm:22s} {np.median(cyc[:, i]):10.0f} cyc  {np.median(cyc[:, i] / tot) * 100:5.1f} %")
 
+    print(f"  {'(hyper: harvest + stats)':22s} {np.median(cyc[:, 19]):10.0f} cyc  "
+          f"{np.median(cyc[:, 19] / tot) * 100:5.1f} %")
     for i, nm in ((16, "red-noise lnL evaluations"), (17, "two-wave rounds"),
                   (18, "accepted red-noise proposals")):
         print(f"  {nm:30s} {cyc[:, i].mean():6.2f} per sweep")
