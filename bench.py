@@ -156,6 +156,7 @@ def workload(config: int, rank: int, world: int, chains: int | None):
         ds = np.repeat(np.arange(len(mine)), per_entry).astype(np.int32)
         return dict(ptas=[e.pta for e in mine], cfgs=[e.cfg for e in mine], ds=ds, init=init,
                     chain0=e0 * per_entry, C=C, per=per_entry, dsid=(e0 + ds).astype(np.int64),
+                    groups_all=np.array([e.model for e in grid]),
                     desc=(f"run_sims.py grid: {CONFIG4_DATASETS} simulated datasets (theta "
                           "0.05/0.1/0.15, Gaussian and Student-t nu=4 white noise, outlier + "
                           "no_outlier twins, 5 outlier models) x 64 chains, datasets sharded "
@@ -309,25 +310,47 @@ class StubSampler:
 
 # ------------------------------------------------------------------------------------------
 def global_diagnostics(draws: np.ndarray, theta: np.ndarray, dsid: np.ndarray,
-                       names: list[str], theta_on: np.ndarray):
+                       names: list[str], theta_on: np.ndarray, groups=None):
     """Split-R-hat and bulk-ESS over ALL gathered chains.  ``draws`` [C, S, P], ``theta``
     [C, S], ``dsid`` [C] (dataset of each chain: chains of one dataset share a posterior),
     ``theta_on`` [ndatasets] (theta is updated by the dataset's model).  ESS is summed over
-    datasets, R-hat maximised over them."""
+    datasets, R-hat maximised over them; with ``groups`` [ndatasets] (e.g. the outlier model
+    of each run_sims entry) the same sums / maxima per group are returned too."""
     from gibbs_student_t_amd import diag
     keys = names + ["theta"]
     ess = {k: 0.0 for k in keys}
     rhat = {k: 0.0 for k in keys}
+    by = {}
     for d in np.unique(dsid):
         sel = dsid == d
         series = {nm: draws[sel, :, j] for j, nm in enumerate(names)}
         if theta_on[d]:
             series["theta"] = theta[sel]
+        g = by.setdefault(str(groups[d]), ({k: 0.0 for k in keys}, {k: 0.0 for k in keys})) \
+            if groups is not None else None
         for k, v in series.items():
             e, r = diag.ess_rhat(v)
-            ess[k] += e if np.isfinite(e) else 0.0
-            rhat[k] = max(rhat[k], r if np.isfinite(r) else np.inf)
-    return ess, rhat
+            e = e if np.isfinite(e) else 0.0
+            r = r if np.isfinite(r) else np.inf
+            ess[k] += e
+            rhat[k] = max(rhat[k], r)
+            if g is not None:
+                g[0][k] += e
+                g[1][k] = max(g[1][k], r)
+    if groups is None:
+        return ess, rhat
+    return ess, rhat, by
+
+
+def ess_rate(ess, rhat, seconds):
+    """ESS/s of the slowest-mixing parameter, or (None, reason) when any R-hat > RHAT_OK."""
+    bad = {k: v for k, v in rhat.items() if not v <= RHAT_OK and ess.get(k, 0) > 0}
+    pos = [v for v in ess.values() if v > 0]
+    if bad:
+        return None, f"R-hat > {RHAT_OK} after the window's burn-in: {bad}"
+    if pos and seconds > 0:
+        return float(min(pos)) / seconds, None
+    return None, "n/a"
 
 
 def main():
@@ -421,7 +444,7 @@ def main():
 
     # ---- ESS window: its own burn-in (discarded) and recorded window, timed on its own
     names = [p.name.split("_", 1)[1] for p in wl["ptas"][0].params]
-    ess = rhat = None
+    ess = rhat = by_group = None
     win_s = 0.0
     if ess_win > 0:
         if ess_burn > 0:
@@ -435,8 +458,11 @@ def main():
         if rank == 0:
             _, allcfgs = config_datasets(args.config) if args.config == 4 else (None, wl["cfgs"])
             theta_on = np.array([c["model"] in ("mixture", "vvh17") for c in allcfgs])
-            ess, rhat = global_diagnostics(draws[..., :-1], draws[..., -1], dsid, names,
-                                           theta_on)
+            groups = wl.get("groups_all")
+            res = global_diagnostics(draws[..., :-1], draws[..., -1], dsid, names, theta_on,
+                                     groups)
+            ess, rhat = res[0], res[1]
+            by_group = res[2] if groups is not None else None
         del wrec, draws
     shards = dist.gather_chains(np.array([[c0, c0 + C]], dtype=np.float64), dev)
     m_vec = np.array([elapsed, kernel_ms, win_s])
@@ -492,13 +518,8 @@ def main():
         if ess is None:
             reason = "no ESS window (config 5: 155 ms per sweep)" if ess_win <= 0 else "n/a"
         else:
-            bad = {k: v for k, v in rhat.items() if not v <= RHAT_OK and ess.get(k, 0) > 0}
-            pos = [v for v in ess.values() if v > 0]
-            if bad:
-                reason = f"R-hat > {RHAT_OK} after the window's burn-in: {bad}"
-            elif pos and win_s > 0:
-                # ESS over every chain of the job / the window's wall time (max over ranks)
-                ess_ps = float(min(pos)) / win_s
+            # ESS over every chain of the job / the window's wall time (max over ranks)
+            ess_ps, reason = ess_rate(ess, rhat, win_s)
         out = {
             "metric": METRIC,
             "value": value,
@@ -520,6 +541,11 @@ def main():
                                       "RCCL only for the final all-gather of chain draws"},
             "ess_per_sec": ess_ps,
             "ess_per_sec_reason": reason,
+            # config 4: the same per outlier model of the run_sims grid (each model's chains
+            # share the window's wall time with the others')
+            "ess_by_model": None if by_group is None else {
+                g: dict(zip(("ess_per_sec", "reason"), ess_rate(e, r, win_s)),
+                        rhat_max=r) for g, (e, r) in sorted(by_group.items())},
             "ess_window": {"burn_in_sweeps": W + K + ess_burn, "sweeps": ess_win, "thin": thin,
                            "seconds": win_s, "chains": C * world,
                            "ess_total": ess, "rhat_max": rhat},
