@@ -45,18 +45,28 @@ def build(force: bool = False, verbose: bool = True, stamps: bool = False,
     """Compile libgst.so (or the diagnostic libgst_stamps.so with per-stage cycle stamps):
     gst.hip (ABI, large path) and one gst_inst.hip object per persistent-kernel shape,
     compiled in parallel, linked into one shared library."""
-    out = STAMPS_LIB if stamps else LIB
-    if not force and not stamps and up_to_date():
+    # experimental variants (not the product library): GST_BUILD_VARIANT=name builds
+    # libgst_<name>.so with GST_EXTRA_CFLAGS added, for A/B timing via GST_LIB
+    variant = os.environ.get("GST_BUILD_VARIANT", "")
+    out = STAMPS_LIB if stamps else (os.path.join(HERE, f"libgst_{variant}.so") if variant else LIB)
+    if not force and not stamps and not variant and up_to_date():
         return LIB
-    objdir = os.path.join(HERE, "_obj_stamps" if stamps else "_obj")
+    objdir = os.path.join(HERE, "_obj_stamps" if stamps else (f"_obj_{variant}" if variant else "_obj"))
     os.makedirs(objdir, exist_ok=True)
     # -amdgpu-mfma-vgpr-form: keep the fp64 MFMA accumulators in VGPRs (gfx950's unified
     # register file); without it hipcc copies all 15 Gram tiles VGPR<->AGPR every k-step.
+    # -disable-machine-licm: the sweep loop body is one huge block; MachineLICM hoists every
+    # loop-invariant fp64 constant (polynomial coefficients of log/exp/cos, ...) and lane
+    # address out of it into VGPRs, and at 256 registers (two chains per SIMD) the allocator
+    # then spills them and reloads them from scratch inside the rejection / MH loops.
+    # Rematerialised in place they cost SALU moves: 576 -> 320 B/lane spill, +7.8% sweeps/s
+    # at 2048 chains (DESIGN.md section 8).
     base = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
-            "-mllvm", "-amdgpu-mfma-vgpr-form",
+            "-mllvm", "-amdgpu-mfma-vgpr-form", "-mllvm", "-disable-machine-licm",
             "-I", os.path.join(ROOT, "include"), "-I", CSRC]
     if stamps:
         base.append("-DGST_STAMPS")
+    base += os.environ.get("GST_EXTRA_CFLAGS", "").split()
     units = [(os.path.join(CSRC, "gst.hip"), [], os.path.join(objdir, "gst.o"))]
     for sh in shapes():
         units.append((os.path.join(CSRC, "gst_inst.hip"), ["-DGST_SHAPE=" + ",".join(sh)],

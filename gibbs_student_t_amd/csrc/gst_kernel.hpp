@@ -158,6 +158,26 @@ __device__ __forceinline__ double rdlane(double v, int lane) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// Per-lane fp64 rows in global memory addressed as (wave-uniform buffer resource, this
+// lane's byte offset, a constant byte offset in an SGPR): every access needs only the one
+// lane-offset VGPR, where 64-bit per-lane pointers (base + lane + 4 KB multiples) would each
+// hold two VGPRs across the sweep loop -- and get spilled, then reloaded one after another.
+struct LaneRows {
+  __amdgpu_buffer_rsrc_t rs;
+  int vo;
+};
+__device__ __forceinline__ LaneRows lane_rows(const double* base, int doubles, int lane) {
+  return {__builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), 0, doubles * 8, 0x00020000),
+          lane * 8};
+}
+__device__ __forceinline__ double lr_load(const LaneRows& b, int byte_off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(b.rs, b.vo, byte_off, 0));
+}
+__device__ __forceinline__ void lr_store(const LaneRows& b, int byte_off, double v) {
+  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), b.rs, b.vo, byte_off, 0);
+}
+
 // Cross-lane moves within a 16-lane row by DPP (VALU speed, no LDS traffic).
 template <int CTRL>
 __device__ __forceinline__ double dpp(double v) {
@@ -701,7 +721,8 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   // the TM factor slots (s < K0) wait in global scratch while the hyper block runs
   // per-chain rows of the state arrays: wave-uniform base pointers (SGPRs), so every
   // per-lane access is base + 32-bit lane offset
-  double* const tmf = st.tmfac + ((size_t)c * (PAIR ? 2 : 1) + role) * NTMS * 64;
+  const LaneRows tmf =
+      lane_rows(st.tmfac + ((size_t)c * (PAIR ? 2 : 1) + role) * NTMS * 64, NTMS * 64, lane);
   double* const xrow = st.x + (size_t)c * md.P;
   double* const brow = st.b + (size_t)c * md.m;
   double* const zrow = st.z + (size_t)c * nst;
@@ -1025,7 +1046,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
 #pragma unroll
     for (int s = 0; s < K0; ++s)
 #pragma unroll
-      for (int r = s; r < MT; ++r) tmf[64 * tm_slot(MT, r, s) + lane] = L[SL(r, s)];
+      for (int r = s; r < MT; ++r) lr_store(tmf, 512 * tm_slot(MT, r, s), L[SL(r, s)]);
   };
 
   // b-marginalised likelihood at xq (gibbs.py:288-329); factor left in L.
@@ -1057,6 +1078,9 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       }
     CholCtx cc{colq, phbuf, lane, p, q, raug, 1.0, 0.0, 0, 0, {tm_apr, 1.0}, {tm_zr, 0.0}};
     GST_SUB_END(7)
+#ifdef GST_EXP_LEAN2
+    if constexpr (OCC == 2) chol_range_lean<MT, K0, RA>(L, cc); else
+#endif
     chol_range<MT, K0, RA>(L, cc);
     GST_SUB_END(8)
     chol_harvest<MT, 8 * K0, RA, RA>(L, cc);
@@ -1465,7 +1489,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
 #pragma unroll
         for (int s = 0; s < K0; ++s)
 #pragma unroll
-          for (int r = s; r < MT; ++r) L[SL(r, s)] = tmf[64 * tm_slot(MT, r, s) + lane];
+          for (int r = s; r < MT; ++r) L[SL(r, s)] = lr_load(tmf, 512 * tm_slot(MT, r, s));
         // y_k = 1/sqrt(a_kk); z = L^-1 d has z_k = zraw_k * y_k; L_ik = a_ik * y_k
 #pragma unroll
         for (int sl = 0; sl < 2; ++sl) {
