@@ -232,8 +232,14 @@ __device__ __forceinline__ void lds_order() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// x[i] as a select chain over register values.  The empty asm makes each element an opaque
+// register value: without it InstCombine turns the select of array loads into a load from a
+// selected address, which keeps the whole parameter array in scratch memory (reloaded in
+// every MH step of the 2-chains-per-SIMD build).
 __device__ __forceinline__ double pget(const double (&x)[4], int i) {
-  return i == 0 ? x[0] : (i == 1 ? x[1] : (i == 2 ? x[2] : x[3]));
+  double a = x[0], b = x[1], c = x[2], d = x[3];
+  asm("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+  return i == 0 ? a : (i == 1 ? b : (i == 2 ? c : d));
 }
 __device__ __forceinline__ int iget4(const int (&a)[4], int i) {
   return i == 0 ? a[0] : (i == 1 ? a[1] : (i == 2 ? a[2] : a[3]));
