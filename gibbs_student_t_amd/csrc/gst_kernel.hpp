@@ -158,6 +158,29 @@ __device__ __forceinline__ double rdlane(double v, int lane) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// Two chains share each SIMD in the OCC = 2 build, and the SIMD's arbiter issues the older
+// wave first: the chain that arrived second ran ~27% slower per sweep than its partner and
+// every launch ended with it (tools/chain_pairs.py).  The two waves take turns at the
+// higher issue priority in time slices of 2^15 clocks, by the parity of their wave slot,
+// checked at the sweep and MH-step boundaries (the clock read waits only there).
+#ifndef GST_PRIO_SHARE
+#define GST_PRIO_SHARE 5   // eighths of the time slot-parity-1 waves hold the higher priority (4: 8.50 M, 5: 8.65 M, 6: 8.38 M chain-sweeps/s: age still favours the older wave)
+#endif
+__device__ __forceinline__ unsigned wave_slot_parity() {
+  return __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4) & 1u;  // HW_REG_HW_ID.WAVE_ID
+}
+template <int OCC>
+__device__ __forceinline__ void fair_prio(unsigned slot) {
+  if constexpr (OCC == 2) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    const bool s1_high = (((unsigned)(t >> 15)) & 7u) < GST_PRIO_SHARE;
+    if (s1_high == (slot != 0u))
+      __builtin_amdgcn_s_setprio(1);
+    else
+      __builtin_amdgcn_s_setprio(0);
+  }
+}
+
 // Per-lane fp64 rows in global memory addressed as (wave-uniform buffer resource, this
 // lane's byte offset, a constant byte offset in an SGPR): every access needs only the one
 // lane-offset VGPR, where 64-bit per-lane pointers (base + lane + 4 KB multiples) would each
@@ -705,6 +728,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   const DevModel& md = mds[ds];
   const int nst = st.nst;
   const int p = lane >> 3, q = lane & 7;
+  const unsigned slotp = OCC == 2 ? wave_slot_parity() : 0u;
   GST_STAMP_DECL
 
   double* S0R = smem[wv];             // S0 during the hyper block, else stage scratch
@@ -1115,6 +1139,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
 
 #pragma unroll 1
   for (int it = 0; it < nsweeps; ++it) {
+    fair_prio<OCC>(slotp);
     rng.sweep = (uint32_t)(sweep0 + it);
     const double* tp = TAPE ? tape.data + ((size_t)c * nsweeps + it) * tape.stride : nullptr;
 
@@ -1241,6 +1266,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       double Qx = exp(2.0 * pget(xv, md.idx_equad) * 2.302585092994045684);
 #pragma unroll 1
       for (int step = -1; step < NWHITE; ++step) {
+        if ((step & 3) == 0) fair_prio<OCC>(slotp);
         double qv[4], luacc = 0.0, Qq = Qx;
         if (step < 0) {
 #pragma unroll
@@ -1431,6 +1457,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       const int first = ((mask & 2u) || eval_only) ? -1 : NHYPER;
 #pragma unroll 1
       for (int step = first; step <= NHYPER; ++step) {
+        fair_prio<OCC>(slotp);
         double qv[4], luacc = 0.0;
         if (step == NHYPER) {
           if (eval_only || !(mask & 4u)) break;
@@ -1612,6 +1639,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     }
 
     GST_STAMP(4)
+    fair_prio<OCC>(slotp);
     // ---- outlier block: theta (gibbs.py:185-198)
     const double ef2 = efac2_of(xv);
     const double Q = exp(2.0 * pget(xv, md.idx_equad) * 2.302585092994045684);
@@ -1631,6 +1659,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         theta = ga / (ga + gb);
       }
     }
+    fair_prio<OCC>(slotp);
     // ---- z (gibbs.py:201-226)
     if ((mask & 16u) && mix) {
       const double SQ2PI = 2.5066282746310002;  // np.sqrt(2*np.pi)
@@ -1664,6 +1693,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         }
       }
     }
+    fair_prio<OCC>(slotp);
     // ---- alpha (gibbs.py:229-242)
     if ((mask & 32u) && md.vary_alpha) {
       int zs = 0;

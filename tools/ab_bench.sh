@@ -5,7 +5,9 @@ set -o pipefail
 mkdir -p gpurun_out/ab
 for lib in "$@"; do
   n=$(basename $lib .so)
-  for a in "--steps 500 --warmup 50" "--steps 20 --warmup 5" "--steps 500 --warmup 50 --chains 1024" "--config 3 --steps 500 --warmup 50"; do
+  CFGS=("--steps 500 --warmup 50" "--steps 20 --warmup 5" "--steps 500 --warmup 50 --chains 1024" "--config 3 --steps 500 --warmup 50")
+  [ -n "$AB_QUICK" ] && CFGS=("--steps 500 --warmup 50" "--steps 20 --warmup 5")
+  for a in "${CFGS[@]}"; do
     tag=$(echo "$a" | tr -d ' -')
     GST_LIB=$lib timeout -k 10 120 python -u bench.py --no-cpu-baseline --ess-window 0 $a \
       > gpurun_out/ab/$n.$tag.json 2> gpurun_out/ab/$n.$tag.err || { echo "FAIL $n $a"; tail -3 gpurun_out/ab/$n.$tag.err; exit 1; }
