@@ -506,7 +506,7 @@ def main():
         traffic = None
         # HBM bytes per chain-sweep of the persistent kernel, PMC (FETCH_SIZE x 2 +
         # WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction) at 2048 chains, 200 sweeps
-        pmc = os.path.join(ROOT, "profiles", "r2_pmc_config2.json")
+        pmc = os.path.join(ROOT, "profiles", "r2b_pmc_config2.json")
         if os.path.exists(pmc) and args.config == 2 and not args.stub:
             try:
                 pj = json.load(open(pmc))
