@@ -458,16 +458,21 @@ struct CholCtx {
 // Every lane stores ("pad, don't mask"): the others' stores go to the junk rows, so the
 // elimination stays free of lane-divergent control flow, which at this register pressure
 // makes the allocator spill kilobytes per lane.
+// The published column carries zeros in its rows <= its own index (slot row s, p <= QQ: the
+// frozen rows and the pivot row), so the readers' row- and column-side multipliers come out
+// masked without a select of their own (one select here instead of two per reader side).
 template <int MT, int QQ>
 __device__ __forceinline__ void chol_publish(const double (&L)[SL(MT, 0)], CholCtx& cc, int s) {
   double* dst = (cc.q == QQ ? cc.colq : cc.junk) + MT * cc.p;
+  const bool live = cc.p > QQ;
 #pragma unroll
   for (int r2 = 0; r2 < MT; r2 += 2) {          // rows (r2, r2+1)
     if (r2 >= s) {  // one ds_write_b128 per row pair (16-byte aligned: MT, r2 even)
       typedef double v2_t __attribute__((ext_vector_type(2)));
-      *(v2_t*)(dst + r2) = (v2_t){L[SL(r2, s)], L[SL(r2 + 1, s)]};
+      const double v0 = (r2 == s) ? (live ? L[SL(r2, s)] : 0.0) : L[SL(r2, s)];
+      *(v2_t*)(dst + r2) = (v2_t){v0, L[SL(r2 + 1, s)]};
     } else if (r2 + 1 >= s)
-      dst[r2 + 1] = L[SL(r2 + 1, s)];
+      dst[r2 + 1] = live ? L[SL(r2 + 1, s)] : 0.0;
   }
 }
 
@@ -527,8 +532,7 @@ __device__ __forceinline__ void chol_step(double (&L)[SL(MT, 0)], CholCtx& cc,
   constexpr int K1 = (KK == 7) ? K + 1 : K;  // slot column of column k+1
   constexpr int KK1 = (KK + 1) & 7;
   constexpr bool NEXT = k + 1 < KEND;
-  cur.lr[K] = (8 * K + cc.p > k) ? cur.lr[K] : 0.0;
-  cur.lc[K] = (8 * K + cc.q > k) ? cur.lc[K] : 0.0;
+  // rows <= k of slot K arrive as zeros (chol_publish): frozen entries stay untouched
   ColView<MT> nxt;
   if constexpr (K1 < MT) {
     // critical path: slot column K1 (holds column k+1).  Its factor a_{8K1+q,k} / a_kk is
@@ -605,8 +609,7 @@ __device__ __forceinline__ void chol_step_lean(double (&L)[SL(MT, 0)], CholCtx& 
   lds_order();
   chol_load<MT, K>(cc, cur);
   pivot_rcp<MT>(cur);
-  cur.lr[K] = (8 * K + cc.p > k) ? cur.lr[K] : 0.0;
-  cur.lc[K] = (8 * K + cc.q > k) ? cur.lc[K] : 0.0;
+  // rows <= k of slot K arrive as zeros (chol_publish): frozen entries stay untouched
   const double sk = fma(cur.y0, cur.e, cur.y0);
 #pragma unroll
   for (int s = K; s < MT; ++s) {
