@@ -43,6 +43,7 @@ struct Ctx {
   int MT = 0, NS = 0, K0 = 0, WPB = 4;
   int ncu = 256;                   // compute units of the device (workgroup sizing)
   double* tmfac = nullptr;         // persistent path: timing-model factor scratch
+  unsigned long long* prog = nullptr;  // persistent path: launch-wide sweep counter (fair_prio)
   size_t tmfac_bytes = 0;
   int path_req = GST_PATH_AUTO;    // gst_set_path
   int path = GST_PATH_PERSISTENT;  // chosen by gst_model_set
@@ -78,6 +79,8 @@ int upload(Ctx* cx, const void* host, size_t bytes, void** dev) {
 
 void free_tmfac(Ctx* cx) {
   if (cx->tmfac) (void)hipFree(cx->tmfac);
+  if (cx->prog) (void)hipFree(cx->prog);
+  cx->prog = nullptr;
   cx->tmfac = nullptr;
   cx->tmfac_bytes = 0;
 }
@@ -563,7 +566,7 @@ static int launch(Ctx* cx, const gst_state* s, const gst_records* r, const gst_t
   if (!s->dataset && cx->nd > 1)
     return fail("gst: the model has several datasets: state.dataset must be set");
   gst::DevState ds{s->x,     s->b,  s->z,      s->alpha,   s->pout, s->theta,
-                   s->nu,    s->status, s->dataset, cx->nmax, cx->nd, nullptr};
+                   s->nu,    s->status, s->dataset, cx->nmax, cx->nd, nullptr, nullptr};
   gst::DevRec dr{};
   if (r) dr = gst::DevRec{r->x, r->b, r->z, r->alpha, r->pout, r->theta, r->nu, r->nrec};
   else record_every = 0;
@@ -595,6 +598,12 @@ static int launch(Ctx* cx, const gst_state* s, const gst_records* r, const gst_t
   ds.tmfac = cx->tmfac;
   const dim3 grid(pair ? C : (C + wpb - 1) / wpb), block(pair ? 128 : 64 * wpb);
   hipStream_t st = (hipStream_t)stream;
+  // two chains per SIMD with every chain resident: the progress rule of fair_prio
+  if (!tape && !pair && C > 4 * cx->ncu && C <= 8 * cx->ncu) {
+    if (!cx->prog) HIP_OK(hipMalloc(&cx->prog, 256));
+    HIP_OK(hipMemsetAsync(cx->prog, 0, sizeof(unsigned long long), st));
+    ds.prog = cx->prog;
+  }
   HIP_OK(hipEventRecord(cx->ev0, st));
   hipLaunchKernelGGL(k, grid, block, 0, st, cx->dmd, ds, dr, dt, C, nsweeps, sweep0,
                      record_every, mask, seed, chain0, eval_only, ow, oh);

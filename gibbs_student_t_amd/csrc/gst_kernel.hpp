@@ -100,6 +100,8 @@ struct DevState {
   int nst;             // row stride of the per-TOA arrays (max n over the datasets)
   int nd;              // number of datasets
   double* tmfac;       // [C][timing-model factor slots][64] scratch (persistent path)
+  unsigned long long* prog;  // chain-sweeps started in this launch (two chains per SIMD, all
+                             // chains resident), or null: see fair_prio
 };
 struct DevRec {
   double *x, *b, *z, *alpha, *pout, *theta, *nu;
@@ -160,21 +162,34 @@ __device__ __forceinline__ double rdlane(double v, int lane) {
 
 // Two chains share each SIMD in the OCC = 2 build, and the SIMD's arbiter issues the older
 // wave first: the chain that arrived second ran ~27% slower per sweep than its partner and
-// every launch ended with it (tools/chain_pairs.py).  The two waves take turns at the
-// higher issue priority in time slices of 2^15 clocks, by the parity of their wave slot,
-// checked at the sweep and MH-step boundaries (the clock read waits only there).
+// every launch ended with it (tools/chain_pairs.py).  Priority turns fix that:
+//  * progress rule (every chain resident): each chain counts its sweep into a launch-wide
+//    counter (one atomic per chain-sweep, its return value consumed steps later); a chain
+//    that has done fewer sweeps than the launch average holds the higher issue priority;
+//  * otherwise, time slices of 2^15 clocks by wave-slot parity (slot-parity-1 waves hold the
+//    higher priority GST_PRIO_SHARE / 8 of the time).
+// Checked at the sweep, MH-step and stage boundaries (the clock read waits only there).
 #ifndef GST_PRIO_SHARE
-#define GST_PRIO_SHARE 5   // eighths of the time slot-parity-1 waves hold the higher priority (4: 8.50 M, 5: 8.65 M, 6: 8.38 M chain-sweeps/s: age still favours the older wave)
+#define GST_PRIO_SHARE 5   // 4: 8.50 M, 5: 8.65 M, 6: 8.38 M chain-sweeps/s (age favours the older wave)
 #endif
 __device__ __forceinline__ unsigned wave_slot_parity() {
   return __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4) & 1u;  // HW_REG_HW_ID.WAVE_ID
 }
+struct Fair {
+  unsigned slot;            // wave-slot parity
+  int behind;               // progress rule: 1 = behind the launch average, -1 = no rule
+};
 template <int OCC>
-__device__ __forceinline__ void fair_prio(unsigned slot) {
+__device__ __forceinline__ void fair_prio(const Fair& f) {
   if constexpr (OCC == 2) {
-    const unsigned long long t = __builtin_amdgcn_s_memtime();
-    const bool s1_high = (((unsigned)(t >> 15)) & 7u) < GST_PRIO_SHARE;
-    if (s1_high == (slot != 0u))
+    bool high;
+    if (f.behind >= 0) {
+      high = f.behind != 0;
+    } else {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      high = ((((unsigned)(t >> 15)) & 7u) < GST_PRIO_SHARE) == (f.slot != 0u);
+    }
+    if (high)
       __builtin_amdgcn_s_setprio(1);
     else
       __builtin_amdgcn_s_setprio(0);
@@ -731,7 +746,8 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   const DevModel& md = mds[ds];
   const int nst = st.nst;
   const int p = lane >> 3, q = lane & 7;
-  const unsigned slotp = OCC == 2 ? wave_slot_parity() : 0u;
+  Fair fair{OCC == 2 ? wave_slot_parity() : 0u, -1};
+  unsigned long long prog_ret = 0ull;  // lane 0: this sweep's ticket from st.prog
   GST_STAMP_DECL
 
   double* S0R = smem[wv];             // S0 during the hyper block, else stage scratch
@@ -1142,7 +1158,19 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
 
 #pragma unroll 1
   for (int it = 0; it < nsweeps; ++it) {
-    fair_prio<OCC>(slotp);
+    if (OCC == 2 && st.prog) {
+      // last sweep's ticket (arrived long ago): behind if fewer sweeps than the average
+      if (it > 0) {
+        const unsigned long long g = __builtin_amdgcn_readfirstlane((unsigned)prog_ret) |
+                                     ((unsigned long long)__builtin_amdgcn_readfirstlane(
+                                          (unsigned)(prog_ret >> 32)) << 32);
+        fair.behind = (unsigned long long)(it - 1) * (unsigned long long)C < g ? 1 : 0;
+      }
+      if (lane == 0)
+        prog_ret = __hip_atomic_fetch_add(st.prog, 1ull, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    }
+    fair_prio<OCC>(fair);
     rng.sweep = (uint32_t)(sweep0 + it);
     const double* tp = TAPE ? tape.data + ((size_t)c * nsweeps + it) * tape.stride : nullptr;
 
@@ -1269,7 +1297,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       double Qx = exp(2.0 * pget(xv, md.idx_equad) * 2.302585092994045684);
 #pragma unroll 1
       for (int step = -1; step < NWHITE; ++step) {
-        if ((step & 3) == 0) fair_prio<OCC>(slotp);
+        if ((step & 3) == 0) fair_prio<OCC>(fair);
         double qv[4], luacc = 0.0, Qq = Qx;
         if (step < 0) {
 #pragma unroll
@@ -1460,7 +1488,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       const int first = ((mask & 2u) || eval_only) ? -1 : NHYPER;
 #pragma unroll 1
       for (int step = first; step <= NHYPER; ++step) {
-        fair_prio<OCC>(slotp);
+        fair_prio<OCC>(fair);
         double qv[4], luacc = 0.0;
         if (step == NHYPER) {
           if (eval_only || !(mask & 4u)) break;
@@ -1642,7 +1670,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     }
 
     GST_STAMP(4)
-    fair_prio<OCC>(slotp);
+    fair_prio<OCC>(fair);
     // ---- outlier block: theta (gibbs.py:185-198)
     const double ef2 = efac2_of(xv);
     const double Q = exp(2.0 * pget(xv, md.idx_equad) * 2.302585092994045684);
@@ -1662,7 +1690,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         theta = ga / (ga + gb);
       }
     }
-    fair_prio<OCC>(slotp);
+    fair_prio<OCC>(fair);
     // ---- z (gibbs.py:201-226)
     if ((mask & 16u) && mix) {
       const double SQ2PI = 2.5066282746310002;  // np.sqrt(2*np.pi)
@@ -1696,7 +1724,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         }
       }
     }
-    fair_prio<OCC>(slotp);
+    fair_prio<OCC>(fair);
     // ---- alpha (gibbs.py:229-242)
     if ((mask & 32u) && md.vary_alpha) {
       int zs = 0;
