@@ -16,15 +16,15 @@ anything touches a GPU and relays rank 0's JSON line.  Chains never communicate 
 sampling; the collectives are the final all-gather of every chain's post-burn-in draws
 (global split-R-hat and bulk-ESS over ALL chains) and a max-reduce of the timings.
 
-Order of a run: W warmup sweeps, then ``--ess-burn`` burn-in sweeps (untimed, discarded),
-then the timed region (K sweeps), then the ESS window.  The timed sweeps therefore measure
-the sampler in its steady state -- chains inside the posterior, as in every sweep a
-production run keeps -- rather than the first sweeps after prior draws (those are ~10%
-slower: DESIGN.md section 8).  ESS/s has its own window, independent of --steps:
-``--ess-window`` sweeps right after the timed region whose sampled parameters and theta are
-recorded every ``--ess-thin``-th sweep, timed on their own; ESS/s = min over quantities of
-the bulk-ESS summed over datasets / window seconds, reported only when every global R-hat
-is <= 1.01 (else null, with the reason).
+Order of a run: W warmup sweeps, the timed region (K sweeps), then ``--ess-burn`` burn-in
+sweeps (untimed, discarded) and the ESS window.  The burn-in runs AFTER the timed region:
+MI355X lowers its shader clock after ~1 s of full load (2.37 -> 2.06 GHz, recovering over
+~20 ms of further work; tools/diag/after_burn.py), so a short timed launch right after a
+long burn-in launch measures the power manager, not the kernel.  ESS/s has its own window,
+independent of --steps: ``--ess-window`` sweeps after the burn-in whose sampled parameters
+and theta are recorded every ``--ess-thin``-th sweep, timed on their own; ESS/s = min over
+quantities of the bulk-ESS summed over datasets / window seconds, reported only when every
+global R-hat is <= 1.01 (else null, with the reason).
 """
 from __future__ import annotations
 
@@ -420,10 +420,7 @@ def main():
     ns.set_state(**wl["init"])
     if W > 0:
         ns.sweep(W, seed=args.seed, sweep0=0, chain0=c0)
-    # burn-in of the ESS window, run before the timed region (untimed, discarded)
     burn = ess_burn if ess_win > 0 else 0
-    if burn > 0:
-        ns.sweep(burn, seed=args.seed, sweep0=W, chain0=c0)
     large = ns.path == "large"
     rec = ns.alloc_records(K, keys=("x", "b", "theta", "nu") if large else
                            ("x", "b", "z", "alpha", "pout", "theta", "nu"))
@@ -442,7 +439,7 @@ def main():
         return time.perf_counter() - t0
 
     # ---- the timed region: exactly K sweeps, every sweep recorded
-    elapsed = timed(lambda: ns.sweep(K, records=rec, seed=args.seed, sweep0=W + burn, chain0=c0))
+    elapsed = timed(lambda: ns.sweep(K, records=rec, seed=args.seed, sweep0=W, chain0=c0))
     kernel_ms = ns.last_kernel_ms()
     ktimes = ns.kernel_times() if large else None
     status = ns.get_state()["status"]
@@ -450,14 +447,16 @@ def main():
     if large:
         ns.set_timing(False)
 
-    # ---- ESS window (after the burn-in and the timed sweeps), timed on its own
+    # ---- ESS window: its own burn-in (discarded) and recorded window, timed on its own
     names = [p.name.split("_", 1)[1] for p in wl["ptas"][0].params]
     ess = rhat = by_group = None
     win_s = 0.0
     if ess_win > 0:
+        if burn > 0:
+            ns.sweep(burn, seed=args.seed, sweep0=W + K, chain0=c0)
         wrec = ns.alloc_records(ess_win // thin, keys=("x", "theta"))
         win_s = timed(lambda: ns.sweep(ess_win, records=wrec, record_every=thin, seed=args.seed,
-                                       sweep0=W + burn + K, chain0=c0))
+                                       sweep0=W + K + burn, chain0=c0))
         draws = dist.gather_chains(torch.cat([wrec["x"], wrec["theta"][..., None]], dim=2)
                                    .cpu().numpy(), dev)
         dsid = dist.gather_chains(wl["dsid"].astype(np.float64), dev).astype(np.int64)
@@ -552,7 +551,7 @@ def main():
             "ess_by_model": None if by_group is None else {
                 g: dict(zip(("ess_per_sec", "reason"), ess_rate(e, r, win_s)),
                         rhat_max=r) for g, (e, r) in sorted(by_group.items())},
-            "ess_window": {"burn_in_sweeps": W + burn + K, "sweeps": ess_win, "thin": thin,
+            "ess_window": {"burn_in_sweeps": W + K + burn, "sweeps": ess_win, "thin": thin,
                            "seconds": win_s, "chains": C * world,
                            "ess_total": ess, "rhat_max": rhat},
             "shards": [[int(a), int(b)] for a, b in shards],   # global chain ids per rank
