@@ -498,6 +498,36 @@ __device__ __forceinline__ double rcp_nr1(double a) {
   return fma(y, fma(-a, y, 1.0), y);
 }
 
+// Per-thread sum of logs as a running product: mantissa product + exponent sum (v_frexp),
+// one log per thread at the end instead of one per TOA (the per-TOA log dominated the white
+// block's 21 likelihood rescans; both paths).  The mantissa product is renormalised every 128 factors
+// (each factor >= 1/2, so it stays far above the fp64 underflow threshold).
+struct LogProd {
+  double mp = 1.0;
+  int ex = 0, k = 0;
+  __device__ __forceinline__ void mul(double v) {
+    int e;
+    mp *= frexp(v, &e);
+    ex += e;
+    if ((++k & 127) == 0) {
+      mp = frexp(mp, &e);
+      ex += e;
+    }
+  }
+  __device__ __forceinline__ double log_sum() const {
+    return log(mp) + (double)ex * 0.693147180559945309417;
+  }
+};
+
+// a / b for positive normal operands without the IEEE division sequence (v_div_scale /
+// v_div_fmas / v_div_fixup): reciprocal estimate, one Newton step, then one residual
+// correction of the quotient (within 1 ulp of the rounded quotient).
+__device__ __forceinline__ double div_pos(double a, double b) {
+  const double y = rcp_nr1(b);
+  const double q0 = a * y;
+  return fma(fma(-b, q0, a), y, q0);
+}
+
 // Raw column k as seen by this lane: rows 8r+p (lr), rows 8r+q (lc), the augmented row
 // entry, the pivot and its reciprocal.
 template <int MT>
@@ -914,16 +944,17 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       sq = wave_sum(sq);
       return -0.5 * (sl + sq);
     }
+    LogProd lp;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       if (vmask & (1u << s)) {
         const double N0 = ef2 * S2(s) + Q;
         const double N = ((zb >> s) & 1u ? al[s] : 1.0) * N0;
-        sl += log(N);
-        sq += yv[s] * yv[s] / N;
+        lp.mul(N);
+        sq += div_pos(yv[s] * yv[s], N);
       }
     }
-    sl = wave_sum(sl);
+    sl = wave_sum(lp.log_sum());
     sq = wave_sum(sq);
     return -0.5 * (sl + sq);
   };
@@ -996,21 +1027,22 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   auto gram_and_tm = [&](const double (&xq)[4]) __attribute__((always_inline)) {
     const double ef2 = efac2_of(xq);
     const double Q = exp(2.0 * pget(xq, md.idx_equad) * 2.302585092994045684);
-    double sl = 0.0, sr = 0.0;
+    double sr = 0.0;
+    LogProd lp;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       const int t = 64 * s + lane;
       double w = 0.0;
       if (vmask & (1u << s)) {
         const double N = ((zb >> s) & 1u ? al[s] : 1.0) * (ef2 * S2(s) + Q);
-        sl += log(N);
+        lp.mul(N);
         const double rs = RR(s);
         sr += rs * rs / N;
         w = 1.0 / N;
       }
       vbuf[t] = w;
     }
-    logdetN = wave_sum(sl);
+    logdetN = wave_sum(lp.log_sum());
     rNr = wave_sum(sr);
     lds_order();
     GST_SUB_BEGIN

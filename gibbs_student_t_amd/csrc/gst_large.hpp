@@ -90,36 +90,6 @@ __device__ __forceinline__ const double* tape_row(const LArgs& a, int c) {
   return a.tape.data ? a.tape.data + ((size_t)c * a.nsweeps + a.it) * a.tape.stride : nullptr;
 }
 
-// Per-thread sum of logs as a running product: mantissa product + exponent sum (v_frexp),
-// one log per thread at the end instead of one per TOA (the per-TOA log dominated the white
-// block's 21 likelihood rescans).  The mantissa product is renormalised every 128 factors
-// (each factor >= 1/2, so it stays far above the fp64 underflow threshold).
-struct LogProd {
-  double mp = 1.0;
-  int ex = 0, k = 0;
-  __device__ __forceinline__ void mul(double v) {
-    int e;
-    mp *= frexp(v, &e);
-    ex += e;
-    if ((++k & 127) == 0) {
-      mp = frexp(mp, &e);
-      ex += e;
-    }
-  }
-  __device__ __forceinline__ double log_sum() const {
-    return log(mp) + (double)ex * 0.693147180559945309417;
-  }
-};
-
-// a / b for positive normal operands without the IEEE division sequence (v_div_scale /
-// v_div_fmas / v_div_fixup): reciprocal estimate, one Newton step, then one residual
-// correction of the quotient (within 1 ulp of the rounded quotient).
-__device__ __forceinline__ double div_pos(double a, double b) {
-  const double y = rcp_nr1(b);
-  const double q0 = a * y;
-  return fma(fma(-b, q0, a), y, q0);
-}
-
 // Deterministic block sum (NW waves): every thread gets the bitwise-identical value.
 template <int NW = 4>
 __device__ __forceinline__ double block_sum(double v, double* red) {
