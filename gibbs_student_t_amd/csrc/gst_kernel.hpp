@@ -26,6 +26,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "philox.hpp"
 
 namespace gst {
@@ -1046,6 +1048,112 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     rNr = wave_sum(sr);
     lds_order();
     GST_SUB_BEGIN
+    if constexpr (PAIR) {
+    // Two waves per chain (PAIR): wave 0 computes the
+    // even Gram tiles, wave 1 the odd ones (each its own MFMA pipe), then the tiles are swapped
+    // through the two waves' stage-scratch regions (4 tiles per wave per round, 2 rounds)
+    // and both waves hold the whole Gram, bitwise the single wave's (same MFMA sequence per
+    // tile).
+    auto gram_tiles = [&](auto own_c) __attribute__((always_inline)) {
+      constexpr int OWN = decltype(own_c)::value;
+      auto mine = [](int T) { return OWN == 0 || (T & 1) == OWN - 1; };
+      v4d acc[NTT];
+#pragma unroll
+      for (int i = 0; i < NTT; ++i) acc[i] = (v4d){0.0, 0.0, 0.0, 0.0};
+      const int tl = lane >> 4;
+      // two k-steps in flight: each operand set is reloaded (for k-step ks + 2) right after
+      // its MFMAs have issued, so a T load has two k-steps (30 MFMAs) to arrive from L2
+      double ta[NT], tb[NT], wa, wb;
+      auto tload = [&](double (&t)[NT], double& w, int ks) __attribute__((always_inline)) {
+        const double* src = md.Tmf + (size_t)ks * NT * 64;
+#pragma unroll
+        for (int X = 0; X < NT; ++X) t[X] = src[X * 64 + lane];
+        w = vbuf[4 * ks + tl];
+      };
+      auto kstep = [&](const double (&t)[NT], const double wt) __attribute__((always_inline)) {
+#pragma unroll
+        for (int I = 0; I < NT; ++I) {
+          const double av = t[I] * wt;
+#pragma unroll
+          for (int J = 0; J <= I; ++J) {
+            const int T = I * (I + 1) / 2 + J;
+            if (mine(T)) acc[T] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, t[J], acc[T], 0, 0, 0);
+          }
+        }
+      };
+      tload(ta, wa, 0);
+      if (md.nks > 1) tload(tb, wb, 1);
+#pragma unroll 1
+      for (int ks = 0; ks < md.nks; ks += 2) {
+        kstep(ta, wa);
+        if (ks + 2 < md.nks) tload(ta, wa, ks + 2);
+        if (ks + 1 < md.nks) {
+          kstep(tb, wb);
+          if (ks + 3 < md.nks) tload(tb, wb, ks + 3);
+        }
+      }
+      GST_SUB_END(9)
+      // MFMA C layout (col = lane&15, row = lane>>4 + 4 reg) -> cyclic register layout
+      if constexpr (OWN == 0) {
+#pragma unroll
+        for (int I = 0; I < NT; ++I) {
+#pragma unroll
+          for (int J = 0; J <= I; ++J) {
+            const v4d a = acc[I * (I + 1) / 2 + J];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) tbuf[(tl + 4 * g) * TB_LD + (lane & 15)] = a[g];
+            lds_order();
+#pragma unroll
+            for (int dr = 0; dr < 2; ++dr)
+#pragma unroll
+              for (int ds = 0; ds < 2; ++ds) {
+                const int r = 2 * I + dr, s = 2 * J + ds;
+                if (r >= s) L[SL(r, s)] = tbuf[(8 * dr + p) * TB_LD + 8 * ds + q];
+              }
+            lds_order();
+          }
+        }
+      } else {
+        constexpr int TS = 16 * TB_LD;  // one padded tile
+        static_assert(4 * TS <= s0r_doubles(MT, K0), "tile swap exceeds the stage scratch");
+#pragma unroll
+        for (int rnd = 0; rnd < 2; ++rnd) {
+#pragma unroll
+          for (int I = 0; I < NT; ++I)
+#pragma unroll
+            for (int J = 0; J <= I; ++J) {
+              const int T = I * (I + 1) / 2 + J;
+              if ((T >> 3) == rnd && mine(T)) {
+                double* dst = smem[OWN - 1] + ((T >> 1) & 3) * TS;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) dst[(tl + 4 * g) * TB_LD + (lane & 15)] = acc[T][g];
+              }
+            }
+          __syncthreads();
+#pragma unroll
+          for (int I = 0; I < NT; ++I)
+#pragma unroll
+            for (int J = 0; J <= I; ++J) {
+              const int T = I * (I + 1) / 2 + J;
+              if ((T >> 3) != rnd) continue;
+              const double* src = smem[T & 1] + ((T >> 1) & 3) * TS;
+#pragma unroll
+              for (int dr = 0; dr < 2; ++dr)
+#pragma unroll
+                for (int ds = 0; ds < 2; ++ds) {
+                  const int r = 2 * I + dr, s = 2 * J + ds;
+                  if (r >= s) L[SL(r, s)] = src[(8 * dr + p) * TB_LD + 8 * ds + q];
+                }
+            }
+          __syncthreads();
+        }
+      }
+    };
+      if (role == 0)
+        gram_tiles(std::integral_constant<int, 1>{});
+      else
+        gram_tiles(std::integral_constant<int, 2>{});
+    } else {
     v4d acc[NTT];
 #pragma unroll
     for (int i = 0; i < NTT; ++i) acc[i] = (v4d){0.0, 0.0, 0.0, 0.0};
@@ -1100,6 +1208,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
           }
         lds_order();
       }
+    }
     }
     // timing-model prior (1/tm_weight) on its diagonal; unit pivots on the pad columns
 #pragma unroll
