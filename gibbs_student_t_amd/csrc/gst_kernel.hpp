@@ -1239,6 +1239,14 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       for (int r = s; r < MT; ++r) lr_store(tmf, 512 * tm_slot(MT, r, s), L[SL(r, s)]);
   };
 
+  // log f_k and log df_k of this lane's Fourier column (f = lane; every instance has
+  // RA - ntm_pad <= 64), held for the launch: loaded from global memory inside every
+  // likelihood they put an L2 round trip in front of each MH step's phi computation
+  static_assert(RA - 8 * K0 <= 64, "one Fourier column per lane");
+  const bool f_live = lane < RA - md.ntm_pad && lane < md.nf;
+  const double lfreq_l = f_live ? md.lfreq[lane] : 0.0;
+  const double ldf_l = f_live ? md.ldf[lane] : 0.0;
+
   // b-marginalised likelihood at xq (gibbs.py:288-329); factor left in L.
   auto lnl_hyper = [&](const double (&xq)[4], int& failed) __attribute__((always_inline)) -> double {
     GST_COUNT(16)
@@ -1249,8 +1257,8 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     const double lc = 2.0 * lA * 2.302585092994045684 - md.log_12pi2 + (g - 3.0) * md.log_fyr;
     // Fourier columns, then the unit-prior dummies that pad a smaller model up to this
     // instance's RA (zero Gram rows: each is eliminated as an exact no-op)
-    for (int f = lane; f < RA - md.ntm_pad; f += 64)
-      phbuf[md.ntm_pad + f] = f < md.nf ? exp(-(lc - g * md.lfreq[f] + md.ldf[f])) : 1.0;
+    if (lane < RA - md.ntm_pad)
+      phbuf[md.ntm_pad + lane] = f_live ? exp(-(lc - g * lfreq_l + ldf_l)) : 1.0;
     // phbuf doubles as the eliminations' junk rows: restore the one other entry read
     // below, the augmented row's (no prior on the residual column)
     if (lane == 63) phbuf[raug] = 0.0;
