@@ -102,8 +102,8 @@ struct DevState {
   int nst;             // row stride of the per-TOA arrays (max n over the datasets)
   int nd;              // number of datasets
   double* tmfac;       // [C][timing-model factor slots][64] scratch (persistent path)
-  unsigned long long* prog;  // chain-sweeps started in this launch (two chains per SIMD, all
-                             // chains resident), or null: see fair_prio
+  unsigned long long* prog;  // chain-sweeps started in this launch (two chains per SIMD), or
+                             // null: see fair_prio
 };
 struct DevRec {
   double *x, *b, *z, *alpha, *pout, *theta, *nu;
@@ -165,11 +165,13 @@ __device__ __forceinline__ double rdlane(double v, int lane) {
 // Two chains share each SIMD in the OCC = 2 build, and the SIMD's arbiter issues the older
 // wave first: the chain that arrived second ran ~27% slower per sweep than its partner and
 // every launch ended with it (tools/chain_pairs.py).  Priority turns fix that:
-//  * progress rule (every chain resident): each chain counts its sweep into a launch-wide
-//    counter (one atomic per chain-sweep, its return value consumed steps later); a chain
-//    that has done fewer sweeps than the launch average holds the higher issue priority;
-//  * otherwise, time slices of 2^15 clocks by wave-slot parity (slot-parity-1 waves hold the
-//    higher priority GST_PRIO_SHARE / 8 of the time).
+//  * progress rule (the host passes st.prog): each chain counts its sweep into a
+//    launch-wide counter (one atomic per chain-sweep, its return value consumed a sweep
+//    later); a chain that has done fewer sweeps than the launch average holds the higher
+//    issue priority;
+//  * the first sweep of a launch, and launches without st.prog: time slices of 2^15 clocks
+//    by wave-slot parity (slot-parity-1 waves hold the higher priority GST_PRIO_SHARE / 8
+//    of the time).
 // Checked at the sweep, MH-step and stage boundaries (the clock read waits only there).
 #ifndef GST_PRIO_SHARE
 #define GST_PRIO_SHARE 5   // 4: 8.50 M, 5: 8.65 M, 6: 8.38 M chain-sweeps/s (age favours the older wave)
