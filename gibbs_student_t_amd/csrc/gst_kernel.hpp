@@ -1278,9 +1278,6 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       }
     CholCtx cc{colq, phbuf, lane, p, q, raug, 1.0, 0.0, 0, 0, {tm_apr, 1.0}, {tm_zr, 0.0}};
     GST_SUB_END(7)
-#ifdef GST_EXP_LEAN2
-    if constexpr (OCC == 2) chol_range_lean<MT, K0, RA>(L, cc); else
-#endif
     chol_range<MT, K0, RA>(L, cc);
     GST_SUB_END(8)
     chol_harvest<MT, 8 * K0, RA, RA>(L, cc);
