@@ -231,7 +231,12 @@ def _free_port():
     return port
 
 
-def launch_ranks(n: int, argv: list[str]) -> int:
+def launch_ranks(n: int, argv: list[str], poll_s: float = 0.2, grace_s: float = 10.0) -> int:
+    """Start N rank processes and relay rank 0's output.  Every child is polled: on the
+    first non-zero exit the siblings are terminated (SIGTERM, SIGKILL after ``grace_s``)
+    and the launcher returns that exit status, instead of leaving the surviving ranks
+    blocked in a collective.  Nothing is exec'd: the ranks are plain children."""
+    import threading
     port = str(_free_port())
     procs = []
     for r in range(n):
@@ -240,11 +245,38 @@ def launch_ranks(n: int, argv: list[str]) -> int:
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
                                       env=env, stdout=subprocess.PIPE if r == 0 else None,
                                       text=True))
-    out, _ = procs[0].communicate()
-    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
-    sys.stdout.write(out)
+    print("bench launcher: rank pids " + " ".join(str(p.pid) for p in procs), file=sys.stderr,
+          flush=True)
+    out: list[str] = []
+    reader = threading.Thread(target=lambda: out.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    failed = 0
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [rc for rc in rcs if rc not in (None, 0)]
+        if bad:
+            failed = abs(bad[0]) or 1
+            break
+        if all(rc == 0 for rc in rcs):
+            break
+        time.sleep(poll_s)
+    if failed:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        deadline = time.time() + grace_s
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        print(f"bench launcher: a rank exited with status {failed}; terminated the others",
+              file=sys.stderr, flush=True)
+    reader.join(timeout=grace_s)
+    sys.stdout.write("".join(out))
     sys.stdout.flush()
-    return max(abs(rc) for rc in rcs)
+    return failed
 
 
 # ------------------------------------------------------------------------------------------
@@ -377,6 +409,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--stub-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-worker", nargs=4, default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.cpu_worker:
@@ -400,6 +433,8 @@ def main():
 
     import torch
     rank, local, world = dist.init("gloo" if args.stub else None)
+    if args.stub and rank == args.stub_fail_rank:
+        return 3                       # launcher test: this rank dies, its peers wait in a collective
     if args.stub:
         dev, Sampler = None, StubSampler
 
@@ -459,8 +494,9 @@ def main():
                                        sweep0=W + K + burn, chain0=c0))
         draws = dist.gather_chains(torch.cat([wrec["x"], wrec["theta"][..., None]], dim=2)
                                    .cpu().numpy(), dev)
-        dsid = dist.gather_chains(wl["dsid"].astype(np.float64), dev).astype(np.int64)
+        dsid = dist.gather_chains(wl["dsid"].astype(np.float64), dev)
         if rank == 0:
+            dsid = dsid.astype(np.int64)
             _, allcfgs = config_datasets(args.config) if args.config == 4 else (None, wl["cfgs"])
             theta_on = np.array([c["model"] in ("mixture", "vvh17") for c in allcfgs])
             groups = wl.get("groups_all")

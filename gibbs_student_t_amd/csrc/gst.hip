@@ -61,9 +61,12 @@ struct Ctx {
   size_t evused = 0;
 };
 
-void free_scratch(Ctx* cx) {
+// Scratch that grows inside a launch call is allocated and freed stream-ordered
+// (hipMallocAsync / hipFreeAsync on the launch's stream): no device synchronisation inside
+// gst_sweep, and a buffer is released only after the work queued before it on that stream.
+void free_scratch(Ctx* cx, hipStream_t st) {
   for (double* p : {cx->ls.G, cx->ls.y, cx->ls.w, cx->ls.sc, cx->ls.v})
-    if (p) (void)hipFree(p);
+    if (p) (void)hipFreeAsync(p, st);
   cx->ls = gst::LScratch{};
   cx->scratch_C = 0;
 }
@@ -77,23 +80,25 @@ int upload(Ctx* cx, const void* host, size_t bytes, void** dev) {
   return 0;
 }
 
-void free_tmfac(Ctx* cx) {
-  if (cx->tmfac) (void)hipFree(cx->tmfac);
-  if (cx->prog) (void)hipFree(cx->prog);
-  cx->prog = nullptr;
+void free_tmfac(Ctx* cx, hipStream_t st) {
+  if (cx->tmfac) (void)hipFreeAsync(cx->tmfac, st);
   cx->tmfac = nullptr;
   cx->tmfac_bytes = 0;
 }
 
+// Model replacement / context teardown (outside any launch): wait for the device, then
+// release everything.
 void free_model(Ctx* cx) {
+  (void)hipDeviceSynchronize();
   for (void* p : cx->allocs) (void)hipFree(p);
   cx->allocs.clear();
   cx->hmd.clear();
   cx->dmd = nullptr;
   cx->nd = 0;
   cx->has_model = false;
-  free_scratch(cx);
-  free_tmfac(cx);
+  free_scratch(cx, nullptr);
+  free_tmfac(cx, nullptr);
+  (void)hipDeviceSynchronize();
 }
 
 using gst::kfn_t;
@@ -154,6 +159,7 @@ int gst_ctx_create(int device, void** ctx) {
   cx->ncu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   HIP_OK(hipEventCreate(&cx->ev0));
   HIP_OK(hipEventCreate(&cx->ev1));
+  HIP_OK(hipMalloc(&cx->prog, 256));   // fair_prio's launch-wide sweep counter
   *ctx = cx;
   return 0;
 }
@@ -163,6 +169,7 @@ int gst_ctx_destroy(void* ctx) {
   if (!cx) return 0;
   (void)hipSetDevice(cx->device);
   free_model(cx);
+  if (cx->prog) (void)hipFree(cx->prog);
   for (hipEvent_t e : cx->evpool) (void)hipEventDestroy(e);
   if (cx->ev0) (void)hipEventDestroy(cx->ev0);
   if (cx->ev1) (void)hipEventDestroy(cx->ev1);
@@ -491,18 +498,18 @@ static int large_ys(const Ctx* cx) {
   return ys;
 }
 
-static int ensure_scratch(Ctx* cx, int C) {
+static int ensure_scratch(Ctx* cx, int C, hipStream_t st) {
   if (C <= cx->scratch_C) return 0;
-  free_scratch(cx);
+  free_scratch(cx, st);
   const gst::DevModel& h = cx->hmd[0];
   const size_t mp = h.mp, npad = large_ys(cx);
-  HIP_OK(hipMalloc(&cx->ls.G, (size_t)C * mp * mp * 8));
-  HIP_OK(hipMalloc(&cx->ls.y, (size_t)C * npad * 8));
-  HIP_OK(hipMalloc(&cx->ls.w, (size_t)C * npad * 8));
-  HIP_OK(hipMalloc(&cx->ls.sc, (size_t)C * 16 * 8));
-  HIP_OK(hipMalloc(&cx->ls.v, (size_t)C * mp * 8));
-  HIP_OK(hipMemset(cx->ls.G, 0, (size_t)C * mp * mp * 8));
-  HIP_OK(hipMemset(cx->ls.v, 0, (size_t)C * mp * 8));
+  HIP_OK(hipMallocAsync((void**)&cx->ls.G, (size_t)C * mp * mp * 8, st));
+  HIP_OK(hipMallocAsync((void**)&cx->ls.y, (size_t)C * npad * 8, st));
+  HIP_OK(hipMallocAsync((void**)&cx->ls.w, (size_t)C * npad * 8, st));
+  HIP_OK(hipMallocAsync((void**)&cx->ls.sc, (size_t)C * 16 * 8, st));
+  HIP_OK(hipMallocAsync((void**)&cx->ls.v, (size_t)C * mp * 8, st));
+  HIP_OK(hipMemsetAsync(cx->ls.G, 0, (size_t)C * mp * mp * 8, st));
+  HIP_OK(hipMemsetAsync(cx->ls.v, 0, (size_t)C * mp * 8, st));
   cx->scratch_C = C;
   return 0;
 }
@@ -513,7 +520,7 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
                         int record_every, unsigned mask, unsigned long long seed,
                         long long chain0, int eval_only, double* ow, double* oh,
                         hipStream_t st) {
-  if (ensure_scratch(cx, C)) return -1;
+  if (ensure_scratch(cx, C, st)) return -1;
   const gst::DevModel& h = cx->hmd[0];
   const int ys = large_ys(cx);
   gst::LArgs a{ds, dr, dt, cx->ls, ys, C, nsweeps, 0, record_every, mask, seed, sweep0, chain0,
@@ -590,19 +597,18 @@ static int launch(Ctx* cx, const gst_state* s, const gst_records* r, const gst_t
   // timing-model factor scratch: [C][waves per chain][slots with s < K0][64] doubles
   const int ntms = cx->MT * (cx->MT + 1) / 2 - (cx->MT - cx->K0) * (cx->MT - cx->K0 + 1) / 2;
   const size_t need = (size_t)C * (pair ? 2 : 1) * ntms * 64 * sizeof(double);
+  hipStream_t st = (hipStream_t)stream;
   if (need > cx->tmfac_bytes) {
-    free_tmfac(cx);
-    HIP_OK(hipMalloc(&cx->tmfac, need));
+    free_tmfac(cx, st);
+    HIP_OK(hipMallocAsync((void**)&cx->tmfac, need, st));
     cx->tmfac_bytes = need;
   }
   ds.tmfac = cx->tmfac;
   const dim3 grid(pair ? C : (C + wpb - 1) / wpb), block(pair ? 128 : 64 * wpb);
-  hipStream_t st = (hipStream_t)stream;
   // two chains per SIMD: the progress rule of fair_prio (with more chains than resident
   // slots, the later workgroups count as behind and the launch's tail shortens: config 4
   // 8.24 -> 8.32 M chain-sweeps/s)
   if (!tape && !pair && C > 4 * cx->ncu) {
-    if (!cx->prog) HIP_OK(hipMalloc(&cx->prog, 256));
     HIP_OK(hipMemsetAsync(cx->prog, 0, sizeof(unsigned long long), st));
     ds.prog = cx->prog;
   }

@@ -170,12 +170,10 @@ __device__ __forceinline__ double rdlane(double v, int lane) {
 //    later); a chain that has done fewer sweeps than the launch average holds the higher
 //    issue priority;
 //  * the first sweep of a launch, and launches without st.prog: time slices of 2^15 clocks
-//    by wave-slot parity (slot-parity-1 waves hold the higher priority GST_PRIO_SHARE / 8
+//    by wave-slot parity (slot-parity-1 waves hold the higher priority kPrioShare / 8
 //    of the time).
 // Checked at the sweep, MH-step and stage boundaries (the clock read waits only there).
-#ifndef GST_PRIO_SHARE
-#define GST_PRIO_SHARE 5   // 4: 8.50 M, 5: 8.65 M, 6: 8.38 M chain-sweeps/s (age favours the older wave)
-#endif
+constexpr unsigned kPrioShare = 5;  // 4: 8.50 M, 5: 8.65 M, 6: 8.38 M chain-sweeps/s (age favours the older wave)
 __device__ __forceinline__ unsigned wave_slot_parity() {
   return __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4) & 1u;  // HW_REG_HW_ID.WAVE_ID
 }
@@ -191,7 +189,7 @@ __device__ __forceinline__ void fair_prio(const Fair& f) {
       high = f.behind != 0;
     } else {
       const unsigned long long t = __builtin_amdgcn_s_memtime();
-      high = ((((unsigned)(t >> 15)) & 7u) < GST_PRIO_SHARE) == (f.slot != 0u);
+      high = ((((unsigned)(t >> 15)) & 7u) < kPrioShare) == (f.slot != 0u);
     }
     if (high)
       __builtin_amdgcn_s_setprio(1);
@@ -588,25 +586,14 @@ __device__ __forceinline__ void chol_step(double (&L)[SL(MT, 0)], CholCtx& cc,
     // one value per lane (lc y0 refined by the Newton term), so the published column
     // feeds this FMA directly: LDS load -> FMA and rcp -> mul -> FMA -> FMA are the two
     // step-to-step chains (the row-scaled lrs below stay off them).
-#ifdef GST_EXP_NOLDS  // timing experiment only: critical column without the LDS operands
-    const double t0 = L[SL(K1, K)] * cur.y0;
-    const double tk = fma(t0, cur.e, t0);
-#pragma unroll
-    for (int r = K1; r < MT; ++r) L[SL(r, K1)] = fma(-L[SL(r, K)], tk, L[SL(r, K1)]);
-#else
     const double t0 = cur.lc[K1] * cur.y0;
     const double tk = fma(t0, cur.e, t0);
 #pragma unroll
     for (int r = K1; r < MT; ++r) L[SL(r, K1)] = fma(-cur.lr[r], tk, L[SL(r, K1)]);
-#endif
     if constexpr (NEXT) {
       lds_order();                   // column k's loads precede its overwrite
       chol_publish<MT, KK1>(L, cc, K1);
-#ifdef GST_EXP_NOPIV  // timing experiment only: pivot chain cut
-      nxt.akk = 2.0;
-#else
       nxt.akk = rdlane(L[SL(K1, K1)], 9 * KK1);
-#endif
       lds_order();
       chol_load<MT, K1>(cc, nxt);
       pivot_rcp<MT>(nxt);
@@ -917,9 +904,11 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     for (int s = 0; s < NS; ++s)
       if ((vmask >> s) & 1u) la += ((zb >> s) & 1u) ? log(al[s]) : 0.0;
     wcls_la = wave_sum(la);
+    // only the TOA slots of this chain's dataset: a ragged batch's shorter datasets have
+    // fewer than 64 NS entries of cidx
     int cls[NS];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) cls[s] = md.cidx[64 * s + lane];
+    for (int s = 0; s < NS; ++s) cls[s] = ((vmask >> s) & 1u) ? md.cidx[64 * s + lane] : -1;
     for (int u = 0; u < md.ncls; ++u) {
       double w = 0.0;
 #pragma unroll

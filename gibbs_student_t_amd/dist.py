@@ -8,9 +8,14 @@ gloo on CPU.
 """
 from __future__ import annotations
 
+import datetime
 import os
 
 import numpy as np
+
+# Finite collective timeout: a rank that dies leaves its peers blocked in a collective;
+# with a finite timeout they fail instead of holding the GPUs until the box's own limit.
+DEFAULT_TIMEOUT_S = float(os.environ.get("GST_DIST_TIMEOUT_S", "300"))
 
 
 def env_rank():
@@ -28,7 +33,8 @@ def init(backend: str | None = None):
         import torch
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    dist.init_process_group(backend=backend, rank=rank, world_size=world)
+    dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=DEFAULT_TIMEOUT_S))
     return rank, local, world
 
 
@@ -51,23 +57,26 @@ def reduce_summary(vec_sum: np.ndarray, vec_max: np.ndarray, device=None):
     return s.cpu().numpy(), m.cpu().numpy()
 
 
-def gather_chains(arr: np.ndarray, device=None) -> np.ndarray:
-    """All-gather per-chain arrays (leading axis = this rank's chains, same shape on
-    every rank) in rank order, i.e. global chain order: the one data collective of a run
-    (SURVEY.md 8e), so R-hat / ESS are computed over ALL chains, not per rank.  On GPU
-    ranks the tensors travel over RCCL (xGMI); one ~C x draws x params fp64 block per rank,
-    once per run."""
+def gather_chains(arr: np.ndarray, device=None):
+    """Gather per-chain arrays (leading axis = this rank's chains, same shape on every
+    rank) to rank 0, in rank order, i.e. global chain order: the one data collective of a
+    run, so R-hat / ESS are computed over ALL chains, not per rank.  Only
+    rank 0 uses the draws, so only rank 0 receives them (a gather, not an all-gather): one
+    ~C x draws x params fp64 block per rank over RCCL (xGMI) on GPU ranks, once per run.
+    Returns the gathered array on rank 0 and None on the other ranks."""
     import torch
     import torch.distributed as dist
     a = np.ascontiguousarray(arr, dtype=np.float64)
     if not (dist.is_available() and dist.is_initialized()):
         return a
-    world = dist.get_world_size()
+    world, rank = dist.get_world_size(), dist.get_rank()
     dev = device if device is not None else torch.device("cpu")
     t = torch.as_tensor(a, device=dev)
-    out = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
-    dist.all_gather_into_tensor(out, t)
-    return out.cpu().numpy()
+    parts = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
+    dist.gather(t, gather_list=parts, dst=0)
+    if rank != 0:
+        return None
+    return torch.cat(parts, dim=0).cpu().numpy()
 
 
 def barrier(device=None):

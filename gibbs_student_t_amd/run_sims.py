@@ -122,8 +122,25 @@ def _grid_on_device(thetas, realisations, models, seed, sigma_out, red_source, d
     return entries
 
 
-def initial_state(entry: Entry, chains: int, gid0: int, seed: int, nst: int):
-    """Prior draw per chain (run_sims.py:111) and the gibbs.py:29-51 latent initial state."""
+# A record is "in the all-outlier state" when at least half of its TOAs are flagged
+# (sum z >= n / 2).  vvh17 chains start there (z = 1 with alpha fixed at 1e10, gibbs.py:44-51:
+# every TOA is effectively removed, b is drawn from its prior, q ~ 1 keeps z = 1).  The
+# reference's chains leave within ~100-200 sweeps only through the error of its SVD draw at
+# cond(Sigma) ~ 1e22 (gibbs.py:169-180); with the exact Cholesky draw a chain can stay for
+# thousands of sweeps (tools/vvh17_protocol.py), so the study reports
+# the fraction of such records per entry and warns when a vvh17 entry keeps any.
+TRAP_WARN_FRAC = 0.01
+
+
+def initial_state(entry: Entry, chains: int, gid0: int, seed: int, nst: int,
+                  vvh17_start: str = "reference"):
+    """Prior draw per chain (run_sims.py:111) and the gibbs.py:29-51 latent initial state.
+
+    ``vvh17_start="clean"`` starts vvh17 chains with no TOA flagged (z = 0) instead of the
+    reference's all-outlier start (z = 1, gibbs.py:50-51), which the exact b draw leaves
+    only slowly (see TRAP_WARN_FRAC above)."""
+    if vvh17_start not in ("reference", "clean"):
+        raise ValueError("vvh17_start must be 'reference' or 'clean'")
     pta, cfg = entry.pta, entry.cfg
     n, m = pta.T.shape
     lo = np.array([p.pmin for p in pta.params])
@@ -131,6 +148,8 @@ def initial_state(entry: Entry, chains: int, gid0: int, seed: int, nst: int):
     x = np.stack([np.random.default_rng([seed, gid0 + c]).uniform(lo, hi)
                   for c in range(chains)])
     z0 = 1.0 if cfg["model"] in ("t", "mixture", "vvh17") else 0.0
+    if cfg["model"] == "vvh17" and vvh17_start == "clean":
+        z0 = 0.0
     a0 = 1.0 if cfg.get("vary_alpha", True) else float(cfg.get("alpha", 1e10))
     z = np.zeros((chains, nst))
     z[:, :n] = z0
@@ -144,7 +163,8 @@ def initial_state(entry: Entry, chains: int, gid0: int, seed: int, nst: int):
 class Study:
     """A batch of entries x ``chains`` chains on one GPU (one NativeSampler)."""
 
-    def __init__(self, entries, chains=1, device=0, seed=1, entry0=0):
+    def __init__(self, entries, chains=1, device=0, seed=1, entry0=0,
+                 vvh17_start="reference"):
         from .native import NativeSampler
         self.entries = list(entries)
         self.chains = int(chains)
@@ -155,10 +175,12 @@ class Study:
         E = len(self.entries)
         self.ns.alloc(E * self.chains, dataset=np.repeat(np.arange(E), self.chains))
         nst = self.ns.n
-        parts = [initial_state(e, self.chains, (self.entry0 + i) * self.chains, self.seed, nst)
+        parts = [initial_state(e, self.chains, (self.entry0 + i) * self.chains, self.seed, nst,
+                               vvh17_start)
                  for i, e in enumerate(self.entries)]
         self.ns.set_state(**{k: np.concatenate([p[k] for p in parts]) for k in parts[0]})
         self.sweeps_done = 0
+        self.trapped = None
 
     @property
     def chain0(self):
@@ -181,6 +203,17 @@ class Study:
                   "pout": (ns.n,), "theta": (), "nu": ()}
         sinks = self._open_sinks(outdir, keys, keep, shapes)
         chunk = max(every, (int(chunk) // every) * every)
+        # all-outlier-state counts of the kept records, per chain (from z when recorded,
+        # else from theta: for vvh17's uniform theta prior theta ~ Beta(sum z + 1, n - sum z
+        # + 1), so theta >= 1/2 is the same state)
+        tdev = ns.tdev
+        import torch
+        n_of = torch.tensor(np.repeat([e.pta.n for e in self.entries], C), device=tdev,
+                            dtype=torch.float64)
+        tmask = (torch.arange(ns.n, device=tdev)[None, :] < n_of[:, None]).to(torch.float64)
+        trap_src = "z" if "z" in keys else ("theta" if "theta" in keys else None)
+        trap_cnt = torch.zeros(E * C, dtype=torch.float64, device=tdev)
+        trap_last = torch.zeros(E * C, dtype=torch.float64, device=tdev)
         t0 = time.perf_counter()
         done, ri = 0, 0
         while done < niter:
@@ -196,13 +229,50 @@ class Study:
                     host = rec[key][:, lo - ri:].cpu().numpy()
                     host = host.reshape((E, C) + host.shape[1:])
                     self._write(sinks, key, host, lo - first)
+                if trap_src == "z":
+                    zs = (rec["z"][:, lo - ri:] * tmask[:, None, :]).sum(-1)
+                    st = (zs >= 0.5 * n_of[:, None]).to(torch.float64)
+                elif trap_src == "theta":
+                    st = (rec["theta"][:, lo - ri:] >= 0.5).to(torch.float64)
+                if trap_src:
+                    trap_cnt += st.sum(1)
+                    trap_last = st[:, -1]
             done += k
             ri += kr
             if progress:
                 progress(done, niter, time.perf_counter() - t0)
         ns.synchronize()
         secs = time.perf_counter() - t0
+        self.trapped = self._trap_summary(trap_src, trap_cnt.cpu().numpy(),
+                                          trap_last.cpu().numpy(), keep)
+        if outdir is not None and self.trapped:
+            with open(os.path.join(outdir, f"trapped_entries_{self.entry0}.json"), "w") as f:
+                json.dump(self.trapped, f, indent=1)
         return self._close_sinks(sinks, outdir), secs
+
+    def _trap_summary(self, src, cnt, last, keep):
+        """Per entry: fraction of kept records (and of chains at the last record) in the
+        all-outlier state; a warning for vvh17 entries above TRAP_WARN_FRAC."""
+        if src is None or keep <= 0:
+            return None
+        E, C = len(self.entries), self.chains
+        out = []
+        for i, e in enumerate(self.entries):
+            frac = float(cnt[i * C:(i + 1) * C].sum() / (C * keep))
+            end = float(last[i * C:(i + 1) * C].mean())
+            row = {"entry": self.entry0 + i, "kind": e.kind, "theta": e.theta, "idx": e.idx,
+                   "model": e.model, "source": src, "trapped_record_frac": frac,
+                   "trapped_chain_frac_end": end}
+            if e.model == "vvh17" and frac > TRAP_WARN_FRAC:
+                row["warning"] = (
+                    f"{frac:.1%} of the kept records sit in the all-outlier start state "
+                    "(sum z >= n/2): the exact b draw leaves gibbs.py's z = 1 start slowly; "
+                    "burn in longer or use vvh17_start='clean' (DESIGN.md section 3)")
+                import sys
+                print(f"run_sims WARNING entry {self.entry0 + i} ({e.kind}, theta={e.theta}, "
+                      f"vvh17): {row['warning']}", file=sys.stderr, flush=True)
+            out.append(row)
+        return out
 
     # ---- record sinks -------------------------------------------------------------------
     def _open_sinks(self, outdir, keys, keep, shapes):
@@ -295,6 +365,9 @@ def main(argv=None):
                     help="draw the grid's datasets in one GPU launch (default) or per "
                          "dataset with NumPy")
     ap.add_argument("--red-source", choices=("powerlaw", "red.txt"), default="powerlaw")
+    ap.add_argument("--vvh17-start", choices=("reference", "clean"), default="reference",
+                    help="vvh17 initial outlier flags: the reference's z = 1 (gibbs.py:50-51) "
+                         "or z = 0 (leaves no chain in the all-outlier state)")
     args = ap.parse_args(argv)
     from . import dist
     rank, local, world = dist.init()
@@ -307,13 +380,17 @@ def main(argv=None):
     if not mine:
         dist.finalize()
         return
-    st = Study(mine, chains=args.chains, device=local, seed=args.seed, entry0=rank * per)
+    st = Study(mine, chains=args.chains, device=local, seed=args.seed, entry0=rank * per,
+               vvh17_start=args.vvh17_start)
     recs, secs = st.run(args.niter, burn=args.burn, outdir=args.outdir, chunk=args.chunk,
                         record_every=args.record_every)
     total = len(mine) * args.chains * args.niter
     print(json.dumps({"rank": rank, "entries": len(mine), "chains": args.chains,
                       "sweeps": args.niter, "seconds": secs,
                       "chain_sweeps_per_s": total / secs}), flush=True)
+    for row in st.trapped or []:
+        if row["trapped_record_frac"] > 0:
+            print(json.dumps({"rank": rank, "trapped": row}), flush=True)
     if recs is not None and rank == 0:
         for row in summarise(mine, recs, args.chains):
             print(json.dumps(row))

@@ -14,7 +14,12 @@
  *    model constants it uploads in gst_model_set and its own scratch.
  *  - `stream` is a hipStream_t (may be NULL = default stream).  No host synchronisation
  *    happens inside gst_sweep; gst_sync() waits for the stream.
- *  - one ctx per device; not re-entrant across threads.
+ *  - one ctx per device; not re-entrant across threads, and used from one stream at a
+ *    time: its scratch (the persistent path's parked timing-model factors and sweep
+ *    counter, the large path's per-chain buffers) is shared by all of its launches and
+ *    indexed by launch-local chain, so two concurrent gst_sweep calls on different streams
+ *    would race on it.  Scratch grows with stream-ordered allocation (hipMallocAsync /
+ *    hipFreeAsync on the launch's stream), never with a device-synchronising hipFree.
  */
 #ifndef GST_H_
 #define GST_H_
@@ -85,11 +90,14 @@ typedef struct gst_model_desc {
 
 /* Per-chain state, device pointers, chain-major.  x[C*P], b[C*m], z/alpha/pout[C*nmax]
  * (nmax = largest n of the model's datasets; TOAs t >= n of a chain's dataset are never
- * touched), theta/nu[C]; status[C] may be NULL (bit 0: Cholesky failure seen in the hyper
- * block, bit 1: b-draw factorisation failed and b was kept, bit 2: dataset index out of
- * range -- the persistent path does not run the chain, the large path runs it on dataset
- * 0; bit 3: large path, the chain's 16-chain group mixes datasets).  dataset[C] gives each chain's dataset index into the
- * batch passed to gst_model_set_batch; it may be NULL when there is one dataset. */
+ * touched), theta/nu[C]; status[C] may be NULL, else flags are OR-ed into it:
+ *   status & 1 (bit 0)  a Cholesky failure was seen in the hyper block (lnL = -inf);
+ *   status & 2 (bit 1)  the b-draw factorisation failed and b was kept;
+ *   status & 4 (bit 2)  dataset index out of range: the persistent path does not run the
+ *                       chain, the large path runs it on dataset 0;
+ *   status & 8 (bit 3)  large path: the chain's aligned 16-chain group mixes datasets.
+ * dataset[C] gives each chain's dataset index into the batch passed to
+ * gst_model_set_batch; it may be NULL when there is one dataset. */
 typedef struct gst_state {
   double* x;
   double* b;
@@ -146,7 +154,7 @@ int gst_model_set(void* ctx, const gst_model_desc* desc);
  * priors and the outlier-model options may differ.  Chains pick their dataset through
  * gst_state.dataset.  On the large path every aligned group of 16 chains must share one
  * dataset (its Gram and T b kernels stage one dataset's T per group); a chain whose group
- * mixes datasets is flagged with status bit 8. */
+ * mixes datasets is flagged with status & 8 (bit 3). */
 int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int ndatasets);
 
 /* Number of datasets, largest n (row stride of per-TOA state/records) and tape stride. */

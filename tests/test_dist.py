@@ -105,3 +105,30 @@ def test_two_rank_bench_workloads_partition_chains():
     ent4, C4 = res[0][4][3], res[0][4][2]
     assert set(ent4[:C4]).isdisjoint(set(ent4[C4:]))          # run_sims entries sharded
     assert sorted(set(ent4)) == list(range(256))              # 128 per rank, 64 chains each
+
+
+def _gather_worker(rank, world, port, out):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    r, _, w = dist.init("gloo")
+    got = dist.gather_chains(np.full((3, 2), float(r)) + np.arange(3)[:, None])
+    out.put((r, None if got is None else got.tolist()))
+    dist.finalize()
+
+
+def test_gather_chains_goes_to_rank0_only():
+    """The chain draws are gathered to rank 0 (the only consumer), not all-gathered."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1] is None
+    want = np.concatenate([np.full((3, 2), 0.0) + np.arange(3)[:, None],
+                           np.full((3, 2), 1.0) + np.arange(3)[:, None]])
+    assert np.array_equal(np.array(res[0]), want)

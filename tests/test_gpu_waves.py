@@ -29,12 +29,12 @@ def _init(ref, C, seed):
                 theta=np.full(C, s0["theta"]), nu=np.full(C, s0["nu"]))
 
 
-def _run(ref, C, S, waves, init, mask=_abi.STAGE_ALL, seed=7, sweep0=3):
+def _run(ref, C, S, waves, init, mask=_abi.STAGE_ALL, seed=7, sweep0=3, chain0=0):
     ns = _native(ref, C, "persistent")
     ns.set_waves(waves)
     ns.set_state(**init)
     rec = ns.alloc_records(S)
-    ns.sweep(S, records=rec, seed=seed, sweep0=sweep0, mask=mask)
+    ns.sweep(S, records=rec, seed=seed, sweep0=sweep0, mask=mask, chain0=chain0)
     out = ns.get_state()
     recs = {k: v.cpu().numpy() for k, v in rec.items()}
     ns.close()
