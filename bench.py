@@ -70,6 +70,47 @@ def executed_flops(n: float, nf: int, ntm: int, m: int) -> dict:
             "total": gram + tm + hyper + solves + tb}
 
 
+def persistent_shape(nf: int, ntm: int):
+    """(MT, K0, RA) of the persistent kernel instance a model runs in (gst.hip kShapes)."""
+    for MT, K0, RA in ((8, 2, 56), (10, 2, 76), (10, 3, 76)):
+        if 8 * K0 >= max(ntm, 1) and RA - 8 * K0 >= nf:
+            return MT, K0, RA
+    return None
+
+
+def gram_mfma_flops(n: int, nf: int, ntm: int) -> float:
+    """fp64 MFMA flops the persistent kernel's Gram executes per chain-sweep: the lower
+    16x16 tiles of the padded augmented system, ceil(n / 4) k-steps of 16x16x4 each."""
+    sh = persistent_shape(nf, ntm)
+    if sh is None:
+        return float("nan")
+    NT = (sh[2] + 1 + 15) // 16
+    return NT * (NT + 1) / 2 * ((n + 3) // 4) * 2 * 16 * 16 * 4
+
+
+def stage_costs(ns, S: int, seed: int, sweep0: int, chain0: int) -> dict:
+    """Per-sweep kernel time (ms, HIP events) of stage-masked persistent launches: nothing
+    (launch + state load/store), the per-TOA pass (white MH + theta, z, alpha, nu), the Gram
+    with the timing-model elimination only (GST_STAGE_GRAM), and the whole red-noise block
+    (Gram + the 11 likelihood factorisations).  Run after the ESS window: they move the
+    chains, which no longer matters then."""
+    from gibbs_student_t_amd import _abi
+    toa = _abi.STAGE_WHITE | _abi.STAGE_THETA | _abi.STAGE_Z | _abi.STAGE_ALPHA | _abi.STAGE_DF
+    out = {}
+    # a full-mask launch first: after host-side work the GPU is ramping its clock back up
+    # from idle, which would be charged to whichever stage launch came first
+    ns.sweep(S, seed=seed, sweep0=sweep0, chain0=chain0)
+    for name, mask in (("fixed", 0), ("toa_pass", toa), ("gram", _abi.STAGE_GRAM),
+                       ("hyper", _abi.STAGE_HYPER)):
+        t = []
+        for rep in range(2):        # the faster of two launches of each
+            ns.sweep(S, seed=seed, sweep0=sweep0, chain0=chain0, mask=mask)
+            ns.synchronize()
+            t.append(ns.last_kernel_ms() / S)
+        out[name] = min(t)
+    return out
+
+
 def toa_pass_bytes(n: float) -> float:
     """Per-TOA pass HBM bytes per chain-sweep: 8 n (6 + 2*21)."""
     return 8.0 * n * (6 + 2 * 21)
@@ -153,7 +194,9 @@ def workload(config: int, rank: int, world: int, chains: int | None):
         e0 = rank * per_rank
         mine = grid[e0:e0 + per_rank]
         nst = max(e.pta.n for e in mine)
-        parts = [run_sims.initial_state(e, per_entry, (e0 + i) * per_entry, 7, nst)
+        # vvh17 entries start as run_sims.Study does by default (z = 0: the reference's z = 1
+        # start is left only after ~1000-5000 sweeps with the exact b draw)
+        parts = [run_sims.initial_state(e, per_entry, (e0 + i) * per_entry, 7, nst, "clean")
                  for i, e in enumerate(mine)]
         init = {k: np.concatenate([p_[k] for p_ in parts]) for k in parts[0]}
         C = len(mine) * per_entry
@@ -175,7 +218,7 @@ def workload(config: int, rank: int, world: int, chains: int | None):
 # same MT19937 stream) timed on host cores, one chain per single-threaded process, on the
 # same workload as --config.
 # ------------------------------------------------------------------------------------------
-def _cpu_worker(config: int, seconds: float, seed: int, slot: int):
+def _cpu_worker(config: int, seconds: float, seed: int, slot: int, out: str | None = None):
     import warnings
 
     from oracle.gibbs_oracle import (LegacyNumpyVariates, Oracle, OutlierModel,
@@ -190,31 +233,74 @@ def _cpu_worker(config: int, seconds: float, seed: int, slot: int):
     st = orc_init(pta, orc.cfg)
     src = LegacyNumpyVariates()
     x = orc.sweep(st, x, src)
+    draws = []
     t0 = time.perf_counter()
     k = 0
     while time.perf_counter() - t0 < seconds:
         x = orc.sweep(st, x, src)
+        draws.append(list(x) + [float(st.theta)])    # x and theta at the end of the sweep
         k += 1
-    print(json.dumps({"sweeps": k, "seconds": time.perf_counter() - t0}))
+    secs = time.perf_counter() - t0
+    if out:
+        np.save(out, np.asarray(draws, dtype=np.float64))
+    print(json.dumps({"sweeps": k, "seconds": secs}))
+
+
+CPU_ESS_BURN_FRAC = 0.2     # the CPU chains' first fifth (from prior draws) is burn-in
+
+
+def cpu_ess(draws: list, per_chain_s: list, names: list[str]):
+    """ESS/s of the CPU chains (config 2 / 3: every process samples the same posterior):
+    rank-normalised bulk-ESS and split-R-hat over all chains, each truncated to the
+    shortest chain, after dropping the first CPU_ESS_BURN_FRAC; ESS/s = min over the
+    sampled parameters and theta of the ESS / the window's wall time (processes run in
+    parallel, so the window takes its share of the slowest process's time)."""
+    from gibbs_student_t_amd import diag
+    S = min(len(d) for d in draws)
+    b = int(CPU_ESS_BURN_FRAC * S)
+    if S - b < 40:
+        return None
+    arr = np.stack([d[b:S] for d in draws])              # [chains, window, P + 1]
+    ess, rhat = {}, {}
+    for j, nm in enumerate(names + ["theta"]):
+        e, r = diag.ess_rhat(arr[:, :, j])
+        ess[nm], rhat[nm] = float(e), float(r)
+    win_s = max(t * (S - b) / len(d) for t, d in zip(per_chain_s, draws))
+    pos = [v for v in ess.values() if v > 0 and np.isfinite(v)]
+    return {"ess_per_sec": (min(pos) / win_s) if pos else None, "window_sweeps": S - b,
+            "window_seconds": win_s, "ess_total": ess, "rhat_max": rhat}
 
 
 def cpu_baseline(config: int, seconds: float, cores: int):
+    import tempfile
     env = dict(os.environ, OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1",
                MKL_NUM_THREADS="1", HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
-    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker",
-                               str(config), str(seconds), str(1000 + i), str(i)], env=env,
-                              stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
-             for i in range(cores)]
-    tot, sweeps = 0.0, 0
-    for p in procs:
-        out, _ = p.communicate(timeout=seconds * 10 + 300)
-        r = json.loads(out.strip().splitlines()[-1])
-        tot += r["sweeps"] / r["seconds"]
-        sweeps += r["sweeps"]
+    with tempfile.TemporaryDirectory() as td:
+        outs = [os.path.join(td, f"chain{i}.npy") for i in range(cores)]
+        procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker",
+                                   str(config), str(seconds), str(1000 + i), str(i), outs[i]],
+                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
+                                  text=True)
+                 for i in range(cores)]
+        tot, sweeps, secs = 0.0, 0, []
+        for p in procs:
+            out, _ = p.communicate(timeout=seconds * 10 + 300)
+            r = json.loads(out.strip().splitlines()[-1])
+            tot += r["sweeps"] / r["seconds"]
+            sweeps += r["sweeps"]
+            secs.append(r["seconds"])
+        ess = None
+        if config in (2, 3):
+            ptas, _ = config_datasets(config)
+            names = [p_.name.split("_", 1)[1] for p_ in ptas[0].params]
+            ess = cpu_ess([np.load(o) for o in outs], secs, names)
     what = {2: "one J1713 mixture chain each", 3: "one config-3 (red.txt) mixture chain each",
             4: "each a chain of a different run_sims grid dataset/model",
             5: "one 100k-TOA m=420 mixture chain each"}[config]
     return {"value": tot, "unit": "chain-sweeps/s", "cores": cores, "kind": "port",
+            "ess_per_sec": ess["ess_per_sec"] if ess else None,
+            "ess": ess if ess else ("n/a: the processes sample different grid datasets"
+                                    if config == 4 else "n/a: no ESS window at this size"),
             "sample": f"config {config}: {cores} single-thread processes x {seconds:.0f} s of "
                       f"the oracle (oracle/gibbs_oracle.py, numpy legacy RNG, bit-exact to "
                       f"gibbs.py), {what}, {sweeps} sweeps total"}
@@ -410,11 +496,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--stub-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
-    ap.add_argument("--cpu-worker", nargs=4, default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-worker", nargs="+", default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.cpu_worker:
-        _cpu_worker(int(args.cpu_worker[0]), float(args.cpu_worker[1]),
-                    int(args.cpu_worker[2]), int(args.cpu_worker[3]))
+        w = args.cpu_worker
+        _cpu_worker(int(w[0]), float(w[1]), int(w[2]), int(w[3]), w[4] if len(w) > 4 else None)
         return 0
 
     from gibbs_student_t_amd import dist
@@ -485,6 +571,7 @@ def main():
     # ---- ESS window: its own burn-in (discarded) and recorded window, timed on its own
     names = [p.name.split("_", 1)[1] for p in wl["ptas"][0].params]
     ess = rhat = by_group = None
+    stage_ms = None
     win_s = 0.0
     if ess_win > 0:
         if burn > 0:
@@ -492,6 +579,9 @@ def main():
         wrec = ns.alloc_records(ess_win // thin, keys=("x", "theta"))
         win_s = timed(lambda: ns.sweep(ess_win, records=wrec, record_every=thin, seed=args.seed,
                                        sweep0=W + K + burn, chain0=c0))
+        if not large and not args.stub:       # while the GPU is at its working clock
+            stage_ms = stage_costs(ns, max(1, min(K, 200)), args.seed, W + K + burn + ess_win,
+                                   c0)
         draws = dist.gather_chains(torch.cat([wrec["x"], wrec["theta"][..., None]], dim=2)
                                    .cpu().numpy(), dev)
         dsid = dist.gather_chains(wl["dsid"].astype(np.float64), dev)
@@ -505,6 +595,8 @@ def main():
             ess, rhat = res[0], res[1]
             by_group = res[2] if groups is not None else None
         del wrec, draws
+    if stage_ms is None and not large and not args.stub:
+        stage_ms = stage_costs(ns, max(1, min(K, 200)), args.seed, W + K + burn + ess_win, c0)
     shards = dist.gather_chains(np.array([[c0, c0 + C]], dtype=np.float64), dev)
     m_vec = np.array([elapsed, kernel_ms, win_s])
     s_vec = np.array([float((status != 0).sum())])
@@ -538,23 +630,66 @@ def main():
             toa = {"kernels": "lg_white + lg_toa (HIP events per launch)", "GBps": gbs,
                    "hbm_frac": gbs / HBM_PEAK_GBS,
                    "bytes_per_chain_sweep": toa_pass_bytes(n_eff)}
-        traffic = None
+        traffic, traffic_src = None, None
         # HBM bytes per chain-sweep of the persistent kernel, PMC (FETCH_SIZE x 2 +
-        # WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction) at 2048 chains, 200 sweeps
-        pmc = os.path.join(ROOT, "profiles", "r2b_pmc_config2.json")
-        if os.path.exists(pmc) and args.config == 2 and not args.stub:
-            try:
-                pj = json.load(open(pmc))
-                traffic = pj["hbm_bytes_per_chain_sweep"] * C * K
-            except Exception:
-                traffic = None
-        pmc5 = os.path.join(ROOT, "profiles", "pmc_config5.json")
-        if large and args.config == 5 and os.path.exists(pmc5):
-            try:   # HBM bytes per Gram launch (PMC passes of tools/run_large.py, same shape)
-                g = json.load(open(pmc5))["kernels"]["lg_gram"]
-                traffic = g["hbm_read_bytes"] + g["hbm_write_bytes"]
-            except Exception:
-                traffic = None
+        # WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction) at 2048 chains: a rocprofv3
+        # --pmc pass of this same command, stored under profiles/ -- NOT measured in this
+        # run (counters need their own profiler pass); the newest profile is used
+        for pf in ("r3_pmc_config2.json", "r2b_pmc_config2.json"):
+            pmc = os.path.join(ROOT, "profiles", pf)
+            if os.path.exists(pmc) and args.config == 2 and not args.stub:
+                try:
+                    pj = json.load(open(pmc))
+                    traffic = pj["hbm_bytes_per_chain_sweep"] * C * K
+                    traffic_src = (f"profiles/{pf}: rocprofv3 PMC pass of bench.py (not this "
+                                   f"run), {pj['hbm_bytes_per_chain_sweep']:.0f} B per "
+                                   "chain-sweep x chains x steps")
+                    break
+                except Exception:
+                    traffic = None
+        for pf in ("r3_pmc_config5.json", "pmc_config5.json"):
+            pmc5 = os.path.join(ROOT, "profiles", pf)
+            if large and args.config == 5 and os.path.exists(pmc5):
+                try:   # HBM bytes per Gram launch (PMC passes of tools/run_large.py, same shape)
+                    g = json.load(open(pmc5))["kernels"]["lg_gram"]
+                    traffic = g["hbm_read_bytes"] + g["hbm_write_bytes"]
+                    traffic_src = f"profiles/{pf}: rocprofv3 PMC passes (not this run), per launch"
+                    break
+                except Exception:
+                    traffic = None
+        stage_rep = None
+        if stage_ms is not None:
+            fx = stage_ms["fixed"]
+            t_toa = max(stage_ms["toa_pass"] - fx, 1e-9)
+            t_gram = max(stage_ms["gram"] - fx, 1e-9)
+            t_hyp = max(stage_ms["hyper"] - fx, 1e-9)
+            gbs = toa_pass_bytes(n_eff) * C / (t_toa * 1e-3) / 1e9
+            toa = {"kernels": "gst_sweep_kernel, stage-masked launch (white MH + theta/z/alpha/"
+                              "nu) minus an empty launch, HIP events, this run",
+                   "ms_per_sweep": t_toa, "GBps": gbs, "hbm_frac": gbs / HBM_PEAK_GBS,
+                   "bytes_per_chain_sweep": toa_pass_bytes(n_eff)}
+            g_alg = n_eff * (m + 1) * (m + 2)
+            g_mf = gram_mfma_flops(int(n), pta0.nfourier, pta0.ntm)
+            h_exe = exe["gram"] + exe["tm_elim"] + exe["hyper_chol"]
+            h_fix = g_alg + 12 * m ** 3 / 3
+            stage_rep = {
+                "source": "stage-masked launches of this run (HIP events), fixed cost "
+                          f"{fx * 1e3:.1f} us/sweep subtracted",
+                "gram": {"ms_per_sweep": t_gram,
+                         "tflops_algorithmic": (g_alg + exe["tm_elim"]) * C / (t_gram * 1e-3) / 1e12,
+                         "mfma_tflops_executed": g_mf * C / (t_gram * 1e-3) / 1e12,
+                         "what": "Gram T^T N^-1 [T|r] (fp64 MFMA 16x16x4) + timing-model "
+                                 "elimination"},
+                "gram_cholesky": {"ms_per_sweep": t_hyp,
+                                  "tflops_executed": h_exe * C / (t_hyp * 1e-3) / 1e12,
+                                  "tflops_fixed_formula": h_fix * C / (t_hyp * 1e-3) / 1e12,
+                                  "what": "whole red-noise block: Gram + 11 likelihood "
+                                          "factorisations"},
+            }
+            for v in stage_rep.values():
+                if isinstance(v, dict):
+                    for k2 in [k for k in v if k.startswith(("tflops", "mfma_tflops"))]:
+                        v[k2.replace("tflops", "frac")] = v[k2] / FP64_PEAK_TFLOPS
         ess_ps, reason = None, None
         if ess is None:
             reason = "no ESS window (config 5: 155 ms per sweep)" if ess_win <= 0 else "n/a"
@@ -593,17 +728,21 @@ def main():
             "shards": [[int(a), int(b)] for a, b in shards],   # global chain ids per rank
             "chains_with_status": int(s_vec[0]),
             "kernel_ms": kernel_ms,
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
+            # the persistent kernel is bound by VALU issue and the latency of the
+            # factorisations' step-to-step LDS hand-offs (PMC: MFMA busy ~11%, VALU ~57% of
+            # issue slots); its roofline is the fp64 peak, which MFMA
+            # and VALU share on MI355X.  The large path's Gram is MFMA-bound.
+            "roofline": {"bound": "mfma" if large else "valu-latency",
+                         "peak_kind": "fp64 dense (MFMA = VALU rate on MI355X)",
+                         "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
-                         "traffic": traffic,
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "lg_gram (per-launch HIP events)" if large else
                                    "gst_sweep_kernel (persistent, whole launch, HIP events)",
                          "algorithmic_flop_per_chain_sweep": algorithmic_flops(n_eff, m),
                          "executed_flop_per_chain_sweep": exe,
-                         "per_toa_pass": toa if toa else
-                         "fused into the persistent kernel (no separate launch to time); "
-                         "stage costs from stage-masked launches in "
-                         "profiles/r2_stage_costs_config2.txt"},
+                         "per_toa_pass": toa,
+                         "stages": stage_rep},
             "cpu_baseline": cpu,
         }
         if stages:

@@ -16,16 +16,22 @@ STAGE_WHITE, STAGE_HYPER, STAGE_B = 1, 2, 4
 STAGE_THETA, STAGE_Z, STAGE_ALPHA, STAGE_DF = 8, 16, 32, 64
 STAGE_ALL = 0x7F
 STAGE_B_FORCE = 0x80
+STAGE_GRAM = 0x100          # timing diagnostic: Gram + timing-model elimination only
 TAPE_WHITE, TAPE_HYPER, TAPE_DELTA = 0, 80, 120
 PATH_AUTO, PATH_PERSISTENT, PATH_LARGE = 0, 1, 2
+DEBUG_POISON = 1
 PATHS = {"auto": PATH_AUTO, "persistent": PATH_PERSISTENT, "large": PATH_LARGE}
 KERNEL_KINDS = ("record", "white", "gram", "tmelim", "hyper", "btm", "tb", "toa")
 
 ABI_VERSION = 2
 EXPORTS = ("gst_version", "gst_tape_stride", "gst_last_error", "gst_ctx_create",
            "gst_ctx_destroy", "gst_model_set", "gst_model_set_batch", "gst_model_info",
-           "gst_sweep", "gst_set_path", "gst_get_path", "gst_set_waves", "gst_set_timing", "gst_kernel_times", "gst_eval_lnlike", "gst_sync",
+           "gst_sweep", "gst_set_path", "gst_get_path", "gst_set_waves", "gst_set_debug", "gst_set_timing", "gst_kernel_times", "gst_eval_lnlike", "gst_sync",
            "gst_last_sweep_ms", "gst_debug_stamps", "gst_simulate")
+
+# diagnostics that older builds (A/B timing of library variants) may lack; calling one on
+# such a build raises AttributeError
+OPTIONAL = ("gst_set_debug",)
 
 _P = ct.POINTER
 _D = _P(ct.c_double)
@@ -106,7 +112,7 @@ def load(path: str | None = None):
     except OSError as e:  # pragma: no cover - depends on the machine
         raise GstNativeError(f"cannot load {p}: {e}") from e
     for name in EXPORTS:
-        if not hasattr(lib, name):
+        if not hasattr(lib, name) and name not in OPTIONAL:
             raise GstNativeError(f"{p} lacks symbol {name}")
     lib.gst_version.restype = ct.c_int
     lib.gst_tape_stride.argtypes = [ct.c_int, ct.c_int]
@@ -125,13 +131,15 @@ def load(path: str | None = None):
     lib.gst_set_path.argtypes = [ct.c_void_p, ct.c_int]
     lib.gst_get_path.argtypes = [ct.c_void_p, _P(ct.c_int)]
     lib.gst_set_waves.argtypes = [ct.c_void_p, ct.c_int]
+    if hasattr(lib, "gst_set_debug"):
+        lib.gst_set_debug.argtypes = [ct.c_void_p, ct.c_int]
     lib.gst_set_timing.argtypes = [ct.c_void_p, ct.c_int]
     lib.gst_kernel_times.argtypes = [ct.c_void_p, _P(ct.c_double), _P(ct.c_int), ct.c_int]
     lib.gst_last_sweep_ms.argtypes = [ct.c_void_p, _P(ct.c_double)]
     lib.gst_debug_stamps.argtypes = [ct.c_void_p, ct.c_void_p]
     lib.gst_simulate.argtypes = [_P(SimDesc), ct.c_void_p]
     for name in EXPORTS:
-        if name != "gst_version":
+        if name != "gst_version" and hasattr(lib, name):
             getattr(lib, name).restype = ct.c_int
     if lib.gst_version() != ABI_VERSION:
         raise GstNativeError(f"{p}: ABI version {lib.gst_version()} != {ABI_VERSION}; rebuild")

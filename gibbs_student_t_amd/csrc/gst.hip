@@ -48,6 +48,7 @@ struct Ctx {
   int path_req = GST_PATH_AUTO;    // gst_set_path
   int path = GST_PATH_PERSISTENT;  // chosen by gst_model_set
   int waves = GST_WAVES_AUTO;      // gst_set_waves
+  int debug = 0;                   // gst_set_debug
   std::vector<void*> allocs;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
@@ -539,18 +540,20 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
     a.it = it;
     if (rec_on && it % record_every == 0) LG_LAUNCH(GST_K_RECORD, gst::lg_record, g_chain, b_chain, 0);
     LG_LAUNCH(GST_K_WHITE, gst::lg_white, g_chain, b_toa, 0);
-    if ((mask & 6u) || eval_only) {
+    if ((mask & (6u | GST_STAGE_GRAM)) || eval_only) {
       if (ev_mark(cx, GST_K_GRAM, st, true)) return -1;
       hipLaunchKernelGGL(gst::lg_gram, g_gram, b_gram, gst::GRAM_LDS * 8, st, cx->dmd, a, nsb,
                          npairs);
       HIP_OK(hipGetLastError());
       if (ev_mark(cx, GST_K_GRAM, st, false)) return -1;
       LG_LAUNCH(GST_K_TMELIM, gst::lg_tmelim, g_chain, b_chain, cx->lds_tm);
-      LG_LAUNCH(GST_K_HYPER, gst::lg_hyper, g_chain, b_chain, cx->lds_hyper);
-      if (eval_only) break;
-      if (mask & 4u) {
-        LG_LAUNCH(GST_K_BTM, gst::lg_btm, g_chain, b_chain, cx->lds_btm);
-        LG_LAUNCH(GST_K_TB, gst::lg_tb, g_tb, b_chain, 0);
+      if (!(mask & GST_STAGE_GRAM)) {   // timing diagnostic: Gram + TM elimination only
+        LG_LAUNCH(GST_K_HYPER, gst::lg_hyper, g_chain, b_chain, cx->lds_hyper);
+        if (eval_only) break;
+        if (mask & 4u) {
+          LG_LAUNCH(GST_K_BTM, gst::lg_btm, g_chain, b_chain, cx->lds_btm);
+          LG_LAUNCH(GST_K_TB, gst::lg_tb, g_tb, b_chain, 0);
+        }
       }
     }
     if (!eval_only && (mask & 0x78u)) LG_LAUNCH(GST_K_TOA, gst::lg_toa, g_chain, b_toa, 0);
@@ -573,7 +576,8 @@ static int launch(Ctx* cx, const gst_state* s, const gst_records* r, const gst_t
   if (!s->dataset && cx->nd > 1)
     return fail("gst: the model has several datasets: state.dataset must be set");
   gst::DevState ds{s->x,     s->b,  s->z,      s->alpha,   s->pout, s->theta,
-                   s->nu,    s->status, s->dataset, cx->nmax, cx->nd, nullptr, nullptr};
+                   s->nu,    s->status, s->dataset, cx->nmax, cx->nd, nullptr, nullptr,
+                   cx->debug};
   gst::DevRec dr{};
   if (r) dr = gst::DevRec{r->x, r->b, r->z, r->alpha, r->pout, r->theta, r->nu, r->nrec};
   else record_every = 0;
@@ -590,7 +594,7 @@ static int launch(Ctx* cx, const gst_state* s, const gst_records* r, const gst_t
     else if (wpb >= 2 && C <= 2 * cx->ncu) wpb = 2;
   }
   // two waves per chain when every chain would otherwise leave a SIMD idle
-  const bool pair = !tape && !eval_only &&
+  const bool pair = !tape && !eval_only && !(mask & GST_STAGE_GRAM) &&
                     (cx->waves == GST_WAVES_TWO || (cx->waves == GST_WAVES_AUTO && C <= 2 * cx->ncu));
   kfn_t k = pick(cx->MT, cx->NS, cx->K0, cx->raug, tape, wpb, C > 4 * cx->ncu, pair);
   if (!k) return fail("gst: no kernel instance");
@@ -672,6 +676,14 @@ int gst_set_waves(void* ctx, int waves) {
   if (!cx) return fail("gst_set_waves: null ctx");
   if (waves < GST_WAVES_AUTO || waves > GST_WAVES_TWO) return fail("gst_set_waves: bad value");
   cx->waves = waves;
+  return 0;
+}
+
+int gst_set_debug(void* ctx, int flags) {
+  Ctx* cx = static_cast<Ctx*>(ctx);
+  if (!cx) return fail("gst_set_debug: null ctx");
+  if (flags & ~GST_DEBUG_POISON) return fail("gst_set_debug: unknown flag");
+  cx->debug = flags;
   return 0;
 }
 

@@ -46,13 +46,24 @@ __host__ __device__ constexpr int SL(int r, int s) { return r * (r + 1) / 2 + s;
 //   colq  [8 * MT]             the one published column of the elimination, [p][r]
 //   mhh   [4 * NHYPER]         hyper-MH variates of the sweep
 //   phbuf [8 * MT]             phi^-1 by internal column
+//   colq2 [8 * (MT - KP_MIN)]  the second published column of the paired tail (rows >= KP)
+// Slot column KP from which the elimination runs in column pairs (chol_pair): two columns
+// per LDS hand-off.  The pair buffers hold rows r >= KP only, at row stride MT - KP (even,
+// for 128-bit accesses); LDS is sized for the earliest start, KP_MIN, which keeps the extra
+// LDS within two chains per SIMD (8 per CU).  kp_for: the one-chain-per-SIMD builds pair
+// from KP_MIN; the 256-register two-chains-per-SIMD build only over its last slot columns
+// (pairing earlier spills there, and its second wave already covers much of the hand-off
+// latency).
+constexpr int KP_MIN = 4;
+__host__ __device__ constexpr int pair_pw(int MT) { return MT - KP_MIN; }
+__host__ __device__ constexpr int kp_for(int OCC) { return OCC == 2 ? 6 : KP_MIN; }
 // index of slot (r, s), s < K0, among the timing-model factor slots (column-major)
 __host__ __device__ constexpr int tm_slot(int MT, int r, int s) {
   return s * MT - s * (s - 1) / 2 + (r - s);
 }
 __host__ __device__ constexpr int s0r_doubles(int MT, int K0) { return 64 * SL(MT - K0, 0); }
 __host__ __device__ constexpr int lds_doubles(int MT, int K0) {
-  return s0r_doubles(MT, K0) + 8 * MT + 4 * NHYPER + 8 * MT;
+  return s0r_doubles(MT, K0) + 8 * MT + 4 * NHYPER + 8 * MT + 8 * pair_pw(MT);
 }
 // chains (waves) per SIMD the LDS allows with 4-chain workgroups: 2 when two workgroups
 // (8 chains) fit a CU's 160 KB
@@ -104,6 +115,7 @@ struct DevState {
   double* tmfac;       // [C][timing-model factor slots][64] scratch (persistent path)
   unsigned long long* prog;  // chain-sweeps started in this launch (two chains per SIMD), or
                              // null: see fair_prio
+  int debug;                 // GST_DEBUG_* flags (gst_set_debug)
 };
 struct DevRec {
   double *x, *b, *z, *alpha, *pout, *theta, *nu;
@@ -461,8 +473,9 @@ __device__ __forceinline__ void gamma_mt_slots(const double (&a)[NS], unsigned a
 // these columns, as mantissa product + exponent sum), sum a_{raug,k}^2 / a_kk (= the
 // d^T Sigma^-1 d contribution) and the failure flag.
 struct CholCtx {
-  double* colq;   // [8][MT] the published column
+  double* colq;   // [8][MT] the published column (paired tail: the even column, [8][PW])
   double* junk;   // [8][MT] where the other lanes' publishing stores land (see chol_publish)
+  double* colq2;  // [8][MT - KP] paired tail: the odd column (rows >= KP)
   int lane, p, q, raug;
   double mant, quad;
   int expo, fail;
@@ -547,11 +560,14 @@ __device__ __forceinline__ void pivot_rcp(ColView<MT>& c) {
   c.e = fma(-c.akk, c.y0, 1.0);
 }
 
-template <int MT, int K>
-__device__ __forceinline__ void chol_load(const CholCtx& cc, ColView<MT>& c) {
-  static_assert(MT % 2 == 0, "128-bit column loads need 16-byte alignment");
-  const double* cr = cc.colq + MT * cc.p;
-  const double* cq = cc.colq + MT * cc.q;
+// Rows >= K of a published column [8][STRIDE] whose first stored row is R0 (the one-column
+// steps: colq, stride MT, R0 = 0; the paired tail: colq / colq2, stride MT - KP, R0 = KP).
+template <int MT, int K, int STRIDE = MT, int R0 = 0>
+__device__ __forceinline__ void chol_load(const double* buf, const CholCtx& cc, ColView<MT>& c) {
+  static_assert(MT % 2 == 0 && STRIDE % 2 == 0 && R0 % 2 == 0 && K >= R0,
+                "128-bit column loads need 16-byte alignment");
+  const double* cr = buf + STRIDE * cc.p - R0;
+  const double* cq = buf + STRIDE * cc.q - R0;
 #pragma unroll
   for (int r2 = 0; r2 < MT; r2 += 2) {          // rows (r2, r2+1)
     if (r2 >= K) {  // 128-bit loads (16-byte aligned: MT, r2 even)
@@ -569,10 +585,131 @@ __device__ __forceinline__ void chol_load(const CholCtx& cc, ColView<MT>& c) {
   }
 }
 
+// ---- Paired tail: two columns per LDS hand-off ------------------------------------------
+// From slot column KP on, columns k and k+1 (k even, both in slot column KB) are
+// published together, column k+1 still RAW with respect to column k.  Every lane applies
+// column k's update to its own copy of column k+1 (one FMA per loaded row, the multiplier
+// tk = a(k+1,k) / a_kk a wave-uniform scalar from the owner lanes' registers), so a hand-off
+// serves two columns: the tail of the elimination is latency-bound on the ~140-cycle
+// write -> read hand-off, and this halves the number of hand-offs.
+// Every matrix element still receives the one-column steps' FMAs, with the same operands, in
+// the same order (including which slot column takes the column-scaled form), and the
+// corrected copy of column k+1 is the expression its owner lanes evaluate in the one-column
+// step: the factor is bitwise that of chol_step alone.
+template <int MT, int QQ, int KP>
+__device__ __forceinline__ void chol_publish_pair(const double (&L)[SL(MT, 0)], CholCtx& cc,
+                                                  int s) {
+  constexpr int PW = MT - KP;
+  const bool even = cc.q == QQ, odd = cc.q == QQ + 1;
+  double* dst = (even ? cc.colq : (odd ? cc.colq2 : cc.junk)) + PW * cc.p - KP;
+  const bool live = cc.p > (odd ? QQ + 1 : QQ);   // zero rows <= the column's own index
+#pragma unroll
+  for (int r2 = KP; r2 < MT; r2 += 2) {
+    if (r2 >= s) {
+      typedef double v2_t __attribute__((ext_vector_type(2)));
+      const double v0 = (r2 == s) ? (live ? L[SL(r2, s)] : 0.0) : L[SL(r2, s)];
+      *(v2_t*)(dst + r2) = (v2_t){v0, L[SL(r2 + 1, s)]};
+    } else if (r2 + 1 >= s)
+      dst[r2 + 1] = live ? L[SL(r2 + 1, s)] : 0.0;
+  }
+}
+
+// Publish columns 8KB + QQ and 8KB + QQ + 1 (slot column KB already updated by every earlier
+// column), load both, and turn the odd one into its value after the even column's update.
+// Returns nothing; n0 / n1 are ready for chol_pair (pivots and reciprocals set).
+template <int MT, int KB, int QQ, int KP>
+__device__ __forceinline__ void pair_handoff(double (&L)[SL(MT, 0)], CholCtx& cc,
+                                             ColView<MT>& n0, ColView<MT>& n1) {
+  constexpr int PW = MT - KP;
+  static_assert(QQ % 2 == 0 && KB >= KP && KP % 2 == 0 && KP >= KP_MIN,
+                "pairs start at even columns of the paired tail");
+  lds_order();                       // the previous pair's loads precede the overwrite
+  chol_publish_pair<MT, QQ, KP>(L, cc, KB);
+  const double a22 = rdlane(L[SL(KB, KB)], 9 * QQ);       // a(k, k)
+  const double a32 = rdlane(L[SL(KB, KB)], 9 * QQ + 8);   // a(k+1, k)
+  const double a33 = rdlane(L[SL(KB, KB)], 9 * QQ + 9);   // a(k+1, k+1), before column k
+  lds_order();
+  ColView<MT> raw;
+  chol_load<MT, KB, PW, KP>(cc.colq, cc, n0);
+  chol_load<MT, KB, PW, KP>(cc.colq2, cc, raw);
+  n0.akk = a22;
+  pivot_rcp<MT>(n0);
+  // the one-column step's factor of column k+1's owner lanes (lc[K1] y0 refined)
+  const double t = a32 * n0.y0;
+  const double tk = fma(t, n0.e, t);
+  n1.akk = fma(-a32, tk, a33);
+  pivot_rcp<MT>(n1);
+#pragma unroll
+  for (int r = KB; r < MT; ++r) {
+    n1.lr[r] = fma(-n0.lr[r], tk, raw.lr[r]);
+    n1.lc[r] = fma(-n0.lc[r], tk, raw.lc[r]);
+  }
+  // rows <= k+1 of slot KB: frozen / pivot rows of column k+1, as its publication would carry
+  n1.lr[KB] = (cc.p > QQ + 1) ? n1.lr[KB] : 0.0;
+  n1.lc[KB] = (cc.q > QQ + 1) ? n1.lc[KB] : 0.0;
+}
+
+// Columns k = 8K + KK and k+1 (KK even); c0 / c1 as pair_handoff leaves them.
+template <int MT, int K, int KK, int KEND, int KP>
+__device__ __forceinline__ void chol_pair(double (&L)[SL(MT, 0)], CholCtx& cc, ColView<MT>& c0,
+                                          ColView<MT>& c1) {
+  static_assert(KK % 2 == 0, "pairs start at even columns");
+  constexpr int k = 8 * K + KK;
+  constexpr int KB = (KK == 6) ? K + 1 : K;   // slot column of columns k+2, k+3
+  constexpr int QB = (KK + 2) & 7;
+  constexpr bool NEXT = k + 2 < KEND;
+  static_assert(k + 2 <= KEND, "the paired tail covers an even number of columns");
+  // column k's column-scaled factor (its "critical" slot column is K, which holds k+1)
+  const double t0 = c0.lc[K] * c0.y0;
+  const double tk0 = fma(t0, c0.e, t0);
+  const double sk0 = fma(c0.y0, c0.e, c0.y0);
+  // column k+1's (its critical slot column is KB, which holds k+2)
+  const double t1 = c1.lc[KB < MT ? KB : K] * c1.y0;
+  const double tk1 = fma(t1, c1.e, t1);
+  const double sk1 = fma(c1.y0, c1.e, c1.y0);
+  ColView<MT> n0, n1;
+  if constexpr (KB < MT) {
+    // critical path: slot column KB (columns k+2, k+3) by column k, then by column k+1
+#pragma unroll
+    for (int r = KB; r < MT; ++r) {
+      double v = L[SL(r, KB)];
+      if constexpr (KB == K)
+        v = fma(-c0.lr[r], tk0, v);
+      else
+        v = fma(-(c0.lr[r] * sk0), c0.lc[KB], v);
+      L[SL(r, KB)] = fma(-c1.lr[r], tk1, v);
+    }
+    if constexpr (NEXT) pair_handoff<MT, KB, QB, KP>(L, cc, n0, n1);
+  }
+  // the rest of the two columns' trailing update (row-scaled, as the one-column steps)
+  double lrs0[MT], lrs1[MT];
+#pragma unroll
+  for (int r = K; r < MT; ++r) {
+    lrs0[r] = c0.lr[r] * sk0;
+    lrs1[r] = c1.lr[r] * sk1;
+  }
+#pragma unroll
+  for (int s = K; s < MT; ++s) {
+    if (s == KB) continue;
+#pragma unroll
+    for (int r = s; r < MT; ++r) {
+      if (s == K) {
+        // KK == 6: slot column K is column k's critical one (it holds k+1); column k+1 (the
+        // slot's last) leaves it alone
+        L[SL(r, s)] = fma(-c0.lr[r], tk0, L[SL(r, s)]);
+      } else {
+        const double v = fma(-lrs0[r], c0.lc[s], L[SL(r, s)]);
+        L[SL(r, s)] = fma(-lrs1[r], c1.lc[s], v);
+      }
+    }
+  }
+  if constexpr (NEXT) chol_pair<MT, KB, QB, KEND, KP>(L, cc, n0, n1);
+}
+
 // Step k = 8K + KK, software-pipelined: the slot column holding column k+1 is updated
 // and published first, column k+1's loads and pivot reciprocal are issued, and only then
 // does the rest of step k's trailing update run (covering their latency).
-template <int MT, int K, int KK, int KEND>
+template <int MT, int K, int KK, int KEND, int KP>
 __device__ __forceinline__ void chol_step(double (&L)[SL(MT, 0)], CholCtx& cc,
                                           ColView<MT>& cur) {
   constexpr int k = 8 * K + KK;
@@ -580,7 +717,10 @@ __device__ __forceinline__ void chol_step(double (&L)[SL(MT, 0)], CholCtx& cc,
   constexpr int KK1 = (KK + 1) & 7;
   constexpr bool NEXT = k + 1 < KEND;
   // rows <= k of slot K arrive as zeros (chol_publish): frozen entries stay untouched
-  ColView<MT> nxt;
+  // column k+1 starts the paired tail: publish it together with k+2 (pair_handoff)
+  constexpr bool TOPAIR = NEXT && K1 >= KP;
+  static_assert(!TOPAIR || KK1 == 0, "the paired tail starts at a slot column");
+  ColView<MT> nxt, nxt2;
   if constexpr (K1 < MT) {
     // critical path: slot column K1 (holds column k+1).  Its factor a_{8K1+q,k} / a_kk is
     // one value per lane (lc y0 refined by the Newton term), so the published column
@@ -590,12 +730,14 @@ __device__ __forceinline__ void chol_step(double (&L)[SL(MT, 0)], CholCtx& cc,
     const double tk = fma(t0, cur.e, t0);
 #pragma unroll
     for (int r = K1; r < MT; ++r) L[SL(r, K1)] = fma(-cur.lr[r], tk, L[SL(r, K1)]);
-    if constexpr (NEXT) {
+    if constexpr (TOPAIR) {
+      pair_handoff<MT, K1, 0, KP>(L, cc, nxt, nxt2);
+    } else if constexpr (NEXT) {
       lds_order();                   // column k's loads precede its overwrite
       chol_publish<MT, KK1>(L, cc, K1);
       nxt.akk = rdlane(L[SL(K1, K1)], 9 * KK1);
       lds_order();
-      chol_load<MT, K1>(cc, nxt);
+      chol_load<MT, K1>(cc.colq, cc, nxt);
       pivot_rcp<MT>(nxt);
     }
   }
@@ -612,21 +754,30 @@ __device__ __forceinline__ void chol_step(double (&L)[SL(MT, 0)], CholCtx& cc,
 #pragma unroll
     for (int r = s; r < MT; ++r) L[SL(r, s)] = fma(-lrs[r], cur.lc[s], L[SL(r, s)]);
   }
-  if constexpr (NEXT) chol_step<MT, K1, KK1, KEND>(L, cc, nxt);
+  if constexpr (TOPAIR)
+    chol_pair<MT, K1, 0, KEND, KP>(L, cc, nxt, nxt2);
+  else if constexpr (NEXT)
+    chol_step<MT, K1, KK1, KEND, KP>(L, cc, nxt);
 }
 
 // Eliminate columns [8*KLO, KEND) (compile-time: no branch between steps), updating the
 // trailing slots.
-template <int MT, int KLO, int KEND>
+template <int MT, int KLO, int KEND, int KP>
 __device__ __forceinline__ void chol_range(double (&L)[SL(MT, 0)], CholCtx& cc) {
   static_assert(KEND > 8 * KLO && KEND <= 8 * MT, "bad elimination range");
-  chol_publish<MT, 0>(L, cc, KLO);
-  ColView<MT> c;
-  c.akk = rdlane(L[SL(KLO, KLO)], 0);
-  lds_order();
-  chol_load<MT, KLO>(cc, c);
-  pivot_rcp<MT>(c);
-  chol_step<MT, KLO, 0, KEND>(L, cc, c);
+  if constexpr (KLO >= KP) {
+    ColView<MT> c0, c1;
+    pair_handoff<MT, KLO, 0, KP>(L, cc, c0, c1);
+    chol_pair<MT, KLO, 0, KEND, KP>(L, cc, c0, c1);
+  } else {
+    chol_publish<MT, 0>(L, cc, KLO);
+    ColView<MT> c;
+    c.akk = rdlane(L[SL(KLO, KLO)], 0);
+    lds_order();
+    chol_load<MT, KLO>(cc.colq, cc, c);
+    pivot_rcp<MT>(c);
+    chol_step<MT, KLO, 0, KEND, KP>(L, cc, c);
+  }
   lds_order();
 }
 
@@ -643,7 +794,7 @@ __device__ __forceinline__ void chol_step_lean(double (&L)[SL(MT, 0)], CholCtx& 
   chol_publish<MT, KK>(L, cc, K);
   cur.akk = rdlane(L[SL(K, K)], 9 * KK);
   lds_order();
-  chol_load<MT, K>(cc, cur);
+  chol_load<MT, K>(cc.colq, cc, cur);
   pivot_rcp<MT>(cur);
   // rows <= k of slot K arrive as zeros (chol_publish): frozen entries stay untouched
   const double sk = fma(cur.y0, cur.e, cur.y0);
@@ -775,6 +926,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   double* colq = S0R + S0RD;          // [8][MT] the published column
   double* mhh = colq + 8 * MT;        // [10][4] hyper MH variates
   double* phbuf = mhh + 4 * NHYPER;   // phi^-1 by internal index; eliminations' junk rows
+  double* colq2 = phbuf + 8 * MT;     // [8][PW] paired tail: the odd published column
   double* S0 = S0R + lane;            // S0[64 * slot]
   // scratch inside S0R (S0 is dead outside the hyper block):
   double* mhw = S0R;                  // [20][4] white MH variates (sweep start .. white block)
@@ -1207,7 +1359,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       const int j = 8 * s + q;
       if (p == q) L[SL(s, s)] = (j < md.ntm) ? L[SL(s, s)] + md.tm_phiinv : 1.0;
     }
-    CholCtx cc{colq, phbuf, lane, p, q, raug, 1.0, 0.0, 0, 0, {1.0, 1.0}, {0.0, 0.0}};
+    CholCtx cc{colq, phbuf, colq2, lane, p, q, raug, 1.0, 0.0, 0, 0, {1.0, 1.0}, {0.0, 0.0}};
     GST_SUB_END(10)
     chol_range_lean<MT, 0, 8 * K0>(L, cc);
     chol_harvest<MT, 0, 8 * K0, RA>(L, cc);
@@ -1265,9 +1417,9 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         if (r == s && p == q) v += phbuf[8 * r + p];
         L[SL(r, s)] = v;
       }
-    CholCtx cc{colq, phbuf, lane, p, q, raug, 1.0, 0.0, 0, 0, {tm_apr, 1.0}, {tm_zr, 0.0}};
+    CholCtx cc{colq, phbuf, colq2, lane, p, q, raug, 1.0, 0.0, 0, 0, {tm_apr, 1.0}, {tm_zr, 0.0}};
     GST_SUB_END(7)
-    chol_range<MT, K0, RA>(L, cc);
+    chol_range<MT, K0, RA, kp_for(OCC)>(L, cc);
     GST_SUB_END(8)
     chol_harvest<MT, 8 * K0, RA, RA>(L, cc);
     chol_stats<8 * K0, RA>(cc);
@@ -1310,6 +1462,18 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     fair_prio<OCC>(fair);
     rng.sweep = (uint32_t)(sweep0 + it);
     const double* tp = TAPE ? tape.data + ((size_t)c * nsweeps + it) * tape.stride : nullptr;
+    if (st.debug & 1) {
+      // GST_DEBUG_POISON: between two sweeps a chain's state is exactly what the records
+      // hold (x, b, z, alpha, pout, theta, nu; y = r - T b and the z bits in registers are
+      // functions of it), so every LDS word of the chain and its parked timing-model factor
+      // are dead here.  Overwrite them with a NaN pattern: a sweep that read any of them
+      // before writing it would carry the NaN into its draws, and the chains would no longer
+      // be bitwise those of an ordinary launch (tests/test_gpu_invariants.py).
+      const double poison = __longlong_as_double(0x7ff4dead7ff4deadll);
+      for (int j = lane; j < lds_doubles(MT, K0); j += 64) smem[wv][j] = poison;
+      for (int j = 0; j < NTMS; ++j) lr_store(tmf, 512 * j, poison);
+      lds_order();
+    }
 
     // ---- record the state at the start of the sweep (gibbs.py:355-361)
     if (rec_on && (it % record_every) == 0) {
@@ -1616,13 +1780,14 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
           }
         }
       }
-    } else if ((mask & 6u) || eval_only) {
+    } else if ((mask & (6u | 256u)) || eval_only) {
       gram_and_tm(xv);
       if (fail_tm) status |= 1;
       GST_STAMP(2)
       bool Lvalid = false;
       double l0 = 0.0, p0 = 0.0;
-      const int first = ((mask & 2u) || eval_only) ? -1 : NHYPER;
+      // GST_STAGE_GRAM (256, timing diagnostic): the Gram and the timing-model elimination only
+      const int first = (mask & 256u) ? NHYPER + 1 : (((mask & 2u) || eval_only) ? -1 : NHYPER);
 #pragma unroll 1
       for (int step = first; step <= NHYPER; ++step) {
         fair_prio<OCC>(fair);

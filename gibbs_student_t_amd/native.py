@@ -138,6 +138,12 @@ class NativeSampler:
         code = {"auto": 0, 1: 1, 2: 2}[waves]
         _abi.check(self.lib, self.lib.gst_set_waves(self.ctx, code), "gst_set_waves")
 
+    def set_debug(self, poison: bool = False):
+        """gst_set_debug: GST_DEBUG_POISON overwrites every chain's LDS and parked scratch
+        with NaN at each sweep start (a check that no sweep reads stale state)."""
+        flags = _abi.DEBUG_POISON if poison else 0
+        _abi.check(self.lib, self.lib.gst_set_debug(self.ctx, flags), "gst_set_debug")
+
     # ---- state ---------------------------------------------------------------------
     def alloc(self, C: int, dataset=None):
         """Allocate C chains; ``dataset[c]`` is chain c's dataset index (default all 0)."""

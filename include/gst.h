@@ -51,7 +51,13 @@ enum gst_stage {
   GST_STAGE_ALPHA = 1u << 5, /* update_alpha         gibbs.py:229-242 */
   GST_STAGE_DF = 1u << 6,    /* update_df            gibbs.py:244-259 */
   GST_STAGE_ALL = 0x7fu,
-  GST_STAGE_B_FORCE = 1u << 7 /* draw b regardless of the gibbs.py:373 test (direct call) */
+  GST_STAGE_B_FORCE = 1u << 7, /* draw b regardless of the gibbs.py:373 test (direct call) */
+  /* Timing diagnostic, not a reference stage: compute the Gram T^T N^-1 [T|r] and eliminate
+   * the timing-model columns (the first half of update_hyper_params' first likelihood,
+   * gibbs.py:302-304,321) and nothing else of the red-noise block; the chain state is not
+   * changed by it.  bench.py times it to report the Gram stage's fp64 utilisation.  Always
+   * runs one wave per chain. */
+  GST_STAGE_GRAM = 1u << 8
 };
 
 /* Model + sampler configuration.  Host pointers; copied by gst_model_set.
@@ -198,6 +204,14 @@ int gst_get_path(void* ctx, int* path);
  * always run one wave per chain). */
 enum gst_waves { GST_WAVES_AUTO = 0, GST_WAVES_ONE = 1, GST_WAVES_TWO = 2 };
 int gst_set_waves(void* ctx, int waves);
+
+/* Diagnostics of the persistent path.  GST_DEBUG_POISON: at the start of every sweep each
+ * chain overwrites all of its LDS and its parked timing-model factor scratch with a NaN
+ * pattern; since a chain carries no state between sweeps beyond its state arrays, a launch
+ * with this flag must give bitwise the same chains as one without (a read of any stale word
+ * would surface as NaN / different draws).  Costs time; never set in production. */
+enum gst_debug { GST_DEBUG_POISON = 1 };
+int gst_set_debug(void* ctx, int flags);
 
 /* Per-kernel timing of the large path (HIP events around every launch of the next
  * gst_sweep / gst_eval_lnlike calls while enabled).  gst_kernel_times fills ms[k] (summed

@@ -69,3 +69,32 @@ def test_one_launch_equals_single_sweep_launches(name, build):
                 bad.append((S, k))
     ns.close()
     assert not bad, f"{label}: first difference (sweep, array) {bad[:4]}"
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+@pytest.mark.parametrize("build", ("occ1", "pair", "occ2"))
+def test_poisoned_lds_and_scratch_change_nothing(name, build):
+    """GST_DEBUG_POISON overwrites every chain's LDS (S0 / stage scratch, published columns,
+    junk rows, MH variates, phi^-1) and its parked timing-model factor with NaN at the start
+    of every sweep.  The chains must be bitwise those of an ordinary launch: no sweep reads
+    a word it did not write itself (the stale-LDS hypothesis of VERDICT round 2, item 1)."""
+    label, C, waves = next(b for b in _builds() if b[0] == build)
+    ref = load_ref(name)
+    S, seed, sweep0 = 100, 12, 9
+    init = _init(ref, C, 22)
+    outs = []
+    for poison in (False, True):
+        ns = _native(ref, C, "persistent")
+        ns.set_waves(waves)
+        ns.set_debug(poison=poison)
+        ns.set_state(**init)
+        rec = ns.alloc_records(S)
+        ns.sweep(S, records=rec, seed=seed, sweep0=sweep0)
+        outs.append(({k: v.clone() for k, v in rec.items()},
+                     {k: v.clone() for k, v in ns.state.items()}))
+        ns.close()
+    (r0, s0), (r1, s1) = outs
+    for k in KEYS:
+        assert torch.equal(r0[k], r1[k]), f"{label}: record {k} differs under poisoning"
+    for k in KEYS + ("status",):
+        assert torch.equal(s0[k], s1[k]), f"{label}: final {k} differs under poisoning"

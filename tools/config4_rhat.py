@@ -82,13 +82,16 @@ def main():
                                             "mean_sum_z_end")}))
     print(json.dumps(by_model))
     if worst_npz:
-        mix = [r for r in rows if r["model"] in ("beta", "uniform")]
-        if mix:
-            d = mix[0]["dataset"]
-            sel = wl["ds"] == d
-            np.savez(worst_npz, dataset=d, x=x[sel], theta=th[sel], names=np.array(names),
-                     thin=THIN, first_sweep=W + K + BURN)
-            print("worst mixture dataset", d, "saved to", worst_npz)
+        # the worst 'beta' and the worst 'uniform' dataset: <stem>_d<dataset>.npz each
+        stem = worst_npz[:-4] if worst_npz.endswith(".npz") else worst_npz
+        for mdl in ("beta", "uniform"):
+            mix = [r for r in rows if r["model"] == mdl]
+            if mix:
+                d = mix[0]["dataset"]
+                sel = wl["ds"] == d
+                np.savez(f"{stem}_d{d}.npz", dataset=d, x=x[sel], theta=th[sel],
+                         names=np.array(names), thin=THIN, first_sweep=W + K + BURN)
+                print(f"worst {mdl} dataset", d, "saved to", f"{stem}_d{d}.npz")
 
 
 if __name__ == "__main__":

@@ -1,0 +1,10 @@
+#!/bin/bash
+# round 3: paired tail per instance (KP 4 / 6), poisoning diagnostic, KS/vvh17 protocol tests
+source tools/r3/run_guarded.sh
+O=gpurun_out/r3e; mkdir -p $O
+step 600 $O/bitwise2048.txt python -u tools/ab_bitwise.py gibbs_student_t_amd/libgst_base.so gibbs_student_t_amd/libgst.so 2048 60
+step 600 $O/bitwise1024.txt python -u tools/ab_bitwise.py gibbs_student_t_amd/libgst_base.so gibbs_student_t_amd/libgst.so 1024 60
+step 900 $O/gpu_tests.txt $PYT -m gpu tests/
+step 600 $O/ab.txt bash tools/ab_bench.sh gibbs_student_t_amd/libgst_base.so gibbs_student_t_amd/libgst.so
+cat $O/ab.txt
+step 300 $O/bench_default.txt python -u bench.py
