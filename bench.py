@@ -494,6 +494,9 @@ def main():
                     help="record every k-th sweep of the ESS window (default 5)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stage-costs", action="store_true",
+                    help="skip the stage-masked launches (profiling runs: the timed launch "
+                         "stays the last sweep launch)")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--stub-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-worker", nargs="+", default=None, help=argparse.SUPPRESS)
@@ -579,7 +582,7 @@ def main():
         wrec = ns.alloc_records(ess_win // thin, keys=("x", "theta"))
         win_s = timed(lambda: ns.sweep(ess_win, records=wrec, record_every=thin, seed=args.seed,
                                        sweep0=W + K + burn, chain0=c0))
-        if not large and not args.stub:       # while the GPU is at its working clock
+        if not large and not args.stub and not args.no_stage_costs:   # at the working clock
             stage_ms = stage_costs(ns, max(1, min(K, 200)), args.seed, W + K + burn + ess_win,
                                    c0)
         draws = dist.gather_chains(torch.cat([wrec["x"], wrec["theta"][..., None]], dim=2)
@@ -595,7 +598,7 @@ def main():
             ess, rhat = res[0], res[1]
             by_group = res[2] if groups is not None else None
         del wrec, draws
-    if stage_ms is None and not large and not args.stub:
+    if stage_ms is None and not large and not args.stub and not args.no_stage_costs:
         stage_ms = stage_costs(ns, max(1, min(K, 200)), args.seed, W + K + burn + ess_win, c0)
     shards = dist.gather_chains(np.array([[c0, c0 + C]], dtype=np.float64), dev)
     m_vec = np.array([elapsed, kernel_ms, win_s])

@@ -23,7 +23,7 @@ DEBUG_POISON = 1
 PATHS = {"auto": PATH_AUTO, "persistent": PATH_PERSISTENT, "large": PATH_LARGE}
 KERNEL_KINDS = ("record", "white", "gram", "tmelim", "hyper", "btm", "tb", "toa")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 EXPORTS = ("gst_version", "gst_tape_stride", "gst_last_error", "gst_ctx_create",
            "gst_ctx_destroy", "gst_model_set", "gst_model_set_batch", "gst_model_info",
            "gst_sweep", "gst_set_path", "gst_get_path", "gst_set_waves", "gst_set_debug", "gst_set_timing", "gst_kernel_times", "gst_eval_lnlike", "gst_sync",
@@ -56,6 +56,9 @@ class ModelDesc(ct.Structure):
         ("model", ct.c_int), ("vary_df", ct.c_int), ("vary_alpha", ct.c_int),
         ("theta_prior_beta", ct.c_int), ("mprior", ct.c_double), ("pspin", ct.c_double),
         ("df_A", _D), ("df_B", _D),
+        # ABI 3: general white noise (per-backend parameters, ECORR basis columns)
+        ("nbackend", ct.c_int), ("backend", _I), ("efac_idx", _I), ("equad_idx", _I),
+        ("ecorr_idx", _I), ("n_ecorr", ct.c_int), ("ecorr_backend", _I),
     ]
 
 
@@ -141,7 +144,9 @@ def load(path: str | None = None):
     for name in EXPORTS:
         if name != "gst_version" and hasattr(lib, name):
             getattr(lib, name).restype = ct.c_int
-    if lib.gst_version() != ABI_VERSION:
+    if lib.gst_version() != ABI_VERSION and not os.environ.get("GST_ALLOW_ABI_MISMATCH"):
+        # (A/B timing of an older build of the classic model sets GST_ALLOW_ABI_MISMATCH:
+        # ABI 3 only appended descriptor fields that such a build ignores)
         raise GstNativeError(f"{p}: ABI version {lib.gst_version()} != {ABI_VERSION}; rebuild")
     if path is None:
         _lib = lib

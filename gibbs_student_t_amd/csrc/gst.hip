@@ -185,13 +185,16 @@ int gst_ctx_destroy(void* ctx) {
 static int pack_dataset(Ctx* cx, const gst_model_desc* d, gst::DevModel& md, int ntm_pad,
                         int raug) {
   const int n = d->n, m = d->m, nf = d->nfourier, ntm = d->ntm, P = d->nparams;
+  const int nec = d->n_ecorr;
   const int mpad = round_up(raug + 1, 16);
   const int npad = 64 * ((n + 63) / 64);
 
-  // internal column order: [TM | pad | Fourier | r | pad]
+  // internal column order: [TM | pad | Fourier | ECORR | r | pad]; reference order
+  // [Fourier | TM | ECORR]
   std::vector<int> ref2int(m), int2ref(mpad, -1);
   for (int j = 0; j < nf; ++j) ref2int[j] = ntm_pad + j;
   for (int j = 0; j < ntm; ++j) ref2int[nf + j] = j;
+  for (int j = 0; j < nec; ++j) ref2int[nf + ntm + j] = ntm_pad + nf + j;
   for (int j = 0; j < m; ++j) int2ref[ref2int[j]] = j;
   const int NT = mpad / 16;
   const int nks = round_up(n, 4) / 4;
@@ -303,12 +306,39 @@ static int pack_dataset(Ctx* cx, const gst_model_desc* d, gst::DevModel& md, int
   md.idx_logA = d->idx_log10_A;
   md.idx_gamma = d->idx_gamma;
   md.efac_const = d->efac_const;
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < gst::PMAX; ++j) {
     md.pmin[j] = j < P ? d->pmin[j] : 0.0;
     md.pmax[j] = j < P ? d->pmax[j] : 0.0;
     md.lp_in[j] = j < P ? -std::log(d->pmax[j] - d->pmin[j]) : 0.0;
     md.hind[j] = j < d->n_hyper ? d->hyper_idx[j] : d->hyper_idx[0];
     md.wind[j] = j < d->n_white ? d->white_idx[j] : d->white_idx[0];
+  }
+  // general white noise: per-backend parameter indices, per-TOA backend, ECORR columns
+  const int nb = d->nbackend > 0 ? d->nbackend : 1;
+  md.nb = nb;
+  for (int b = 0; b < gst::NBMAX; ++b) {
+    md.efac_b[b] = b < nb ? (d->efac_idx ? d->efac_idx[b] : d->idx_efac) : -1;
+    md.equad_b[b] = b < nb ? (d->equad_idx ? d->equad_idx[b] : d->idx_equad) : d->idx_equad;
+    md.ecorr_b[b] = b < nb && d->ecorr_idx ? d->ecorr_idx[b] : -1;
+    md.ec_count[b] = 0.0;
+  }
+  md.nec = nec;
+  md.bk = nullptr;
+  md.ecb = nullptr;
+  if (nb > 1) {
+    std::vector<int> bk(npad, 0);
+    for (int t = 0; t < n; ++t) bk[t] = d->backend ? d->backend[t] : 0;
+    if (upload(cx, bk.data(), bk.size() * sizeof(int), &ptr)) return -1;
+    md.bk = (const int*)ptr;
+  }
+  if (nec > 0) {
+    std::vector<int> eb(nec);
+    for (int e = 0; e < nec; ++e) {
+      eb[e] = d->ecorr_backend ? d->ecorr_backend[e] : 0;
+      md.ec_count[eb[e]] += 1.0;
+    }
+    if (upload(cx, eb.data(), eb.size() * sizeof(int), &ptr)) return -1;
+    md.ecb = (const int*)ptr;
   }
   md.lp_sum = 0.0;  // Python sum() order (gibbs.py:339)
   for (int j = 0; j < P; ++j) md.lp_sum += md.lp_in[j];
@@ -347,16 +377,40 @@ static int pack_dataset(Ctx* cx, const gst_model_desc* d, gst::DevModel& md, int
 
 static int check_desc(const gst_model_desc* d) {
   const int n = d->n, m = d->m, nf = d->nfourier, ntm = d->ntm, P = d->nparams;
-  if (n <= 0 || m != nf + ntm || nf <= 0 || ntm < 0) return fail("gst_model_set: bad sizes");
-  if (P < 1 || P > 4) return fail("gst_model_set: nparams must be 1..4");
+  const int nec = d->n_ecorr, nb = d->nbackend > 0 ? d->nbackend : 1;
+  if (n <= 0 || nec < 0 || m != nf + ntm + nec || nf <= 0 || ntm < 0)
+    return fail("gst_model_set: bad sizes");
+  if (P < 1 || P > gst::PMAX) return fail("gst_model_set: nparams must be 1..16");
+  if (nb > gst::NBMAX) return fail("gst_model_set: at most 8 backends");
   if (d->idx_equad < 0 || d->idx_log10_A < 0 || d->idx_gamma < 0)
     return fail("gst_model_set: equad, log10_A and gamma parameters are required");
-  if (d->n_hyper < 1 || d->n_hyper > 4 || d->n_white < 1 || d->n_white > 4)
+  if (d->n_hyper < 1 || d->n_hyper > P || d->n_white < 1 || d->n_white > P)
     return fail("gst_model_set: bad hyper/white index sets");
   if (!d->T || !d->residuals || !d->toaerrs || !d->ffreqs || !d->pmin || !d->pmax ||
       !d->hyper_idx || !d->white_idx || !d->df_A || !d->df_B)
     return fail("gst_model_set: null array in model descriptor");
+  if ((nb > 1 && !d->backend) || (nec > 0 && (!d->ecorr_backend || !d->ecorr_idx)))
+    return fail("gst_model_set: backend / ECORR arrays missing");
+  for (int t = 0; nb > 1 && t < n; ++t)
+    if (d->backend[t] < 0 || d->backend[t] >= nb) return fail("gst_model_set: bad backend index");
+  for (int b = 0; b < nb; ++b) {
+    const int ef = d->efac_idx ? d->efac_idx[b] : d->idx_efac;
+    const int eq = d->equad_idx ? d->equad_idx[b] : d->idx_equad;
+    const int ec = d->ecorr_idx ? d->ecorr_idx[b] : -1;
+    if (ef >= P || eq < 0 || eq >= P || ec >= P) return fail("gst_model_set: bad parameter index");
+  }
+  for (int e = 0; e < nec; ++e) {
+    const int b = d->ecorr_backend[e];
+    if (b < 0 || b >= nb || d->ecorr_idx[b] < 0)
+      return fail("gst_model_set: ECORR column without an ecorr parameter");
+  }
   return 0;
+}
+
+// The classic model of the register-resident kernel: one backend, no ECORR, P <= 4.
+static bool classic(const gst_model_desc* d) {
+  return (d->nbackend <= 1) && d->n_ecorr == 0 && d->nparams <= 4 && d->n_hyper <= 4 &&
+         d->n_white <= 4;
 }
 
 // Datasets of one batch share the sampler structure: basis shape, parameter roles and the
@@ -365,7 +419,8 @@ static int same_structure(const gst_model_desc* a, const gst_model_desc* b) {
   if (a->m != b->m || a->nfourier != b->nfourier || a->ntm != b->ntm ||
       a->nparams != b->nparams || a->idx_efac != b->idx_efac || a->idx_equad != b->idx_equad ||
       a->idx_log10_A != b->idx_log10_A || a->idx_gamma != b->idx_gamma ||
-      a->n_hyper != b->n_hyper || a->n_white != b->n_white)
+      a->n_hyper != b->n_hyper || a->n_white != b->n_white || a->n_ecorr != b->n_ecorr ||
+      (a->nbackend > 1 ? a->nbackend : 1) != (b->nbackend > 1 ? b->nbackend : 1))
     return 0;
   for (int j = 0; j < a->n_hyper; ++j)
     if (a->hyper_idx[j] != b->hyper_idx[j]) return 0;
@@ -387,13 +442,14 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
     nmax = std::max(nmax, descs[i].n);
   }
   const gst_model_desc* d = &descs[0];
-  const int nf = d->nfourier, ntm = d->ntm, m = d->m;
+  const int nf = d->nfourier, ntm = d->ntm, m = d->m, nec = d->n_ecorr;
   const Shape* sh = shape_for(nf, ntm);
   const int MT = sh ? sh->MT : 0, K0 = sh ? sh->K0 : 0;
   const int raug = sh ? sh->RA : 0;
   const int nsl = (nmax + 63) / 64;
   const int NS = nsl <= 2 ? 2 : (nsl <= 3 ? 3 : 4);
-  const bool fits = sh && round_up(nmax, 4) <= 64 * NS && pick(MT, NS, K0, raug, false, 4, false);
+  const bool fits = sh && classic(d) && round_up(nmax, 4) <= 64 * NS &&
+                    pick(MT, NS, K0, raug, false, 4, false);
   int path = cx->path_req;
   if (path == GST_PATH_AUTO) path = fits ? GST_PATH_PERSISTENT : GST_PATH_LARGE;
   if (path == GST_PATH_PERSISTENT && !fits) {
@@ -405,14 +461,15 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
     return fail(b);
   }
   if (path == GST_PATH_LARGE) {
-    const int ms = nf + 1;
-    if ((size_t)(ms * (ms + 1) + nf + 2 * ms) * 8 > 160 * 1024)
-      return fail("gst_model_set: large path needs nfourier <= 138 (LDS-resident Fourier block)");
+    const int ms = nf + nec + 1;
+    if ((size_t)(ms * (ms + 1) + nf + nec + 2 * ms) * 8 > 160 * 1024)
+      return fail("gst_model_set: large path needs nfourier + n_ecorr <= 138 (LDS-resident "
+                  "red-noise / ECORR block)");
   }
   free_model(cx);
   // large path: timing-model block padded to whole 16-column MFMA tiles, no dummies
   const int ntm_pad = path == GST_PATH_LARGE ? round_up(ntm > 0 ? ntm : 1, 16) : 8 * K0;
-  const int raug_pack = path == GST_PATH_LARGE ? ntm_pad + nf : raug;
+  const int raug_pack = path == GST_PATH_LARGE ? ntm_pad + nf + nec : raug;
   std::vector<gst::DevModel> hmd(nd);
   for (int i = 0; i < nd; ++i)
     if (pack_dataset(cx, &descs[i], hmd[i], ntm_pad, raug_pack)) {
@@ -436,8 +493,8 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
     const gst::DevModel& h = hmd[0];
     cx->raug = h.raug;
     cx->lds_tm = (size_t)h.mp * (gst::TM_PW + 1) * 8;
-    const int ms = h.nf + 1;
-    cx->lds_hyper = (size_t)(ms * (ms + 1) + h.nf + 2 * ms) * 8;
+    const int ms = h.nf + h.nec + 1;
+    cx->lds_hyper = (size_t)(ms * (ms + 1) + h.nf + h.nec + 2 * ms) * 8;
     cx->lds_btm = (size_t)(3 * h.ntm_pad + h.raug) * 8;
     HIP_OK(hipFuncSetAttribute((const void*)gst::lg_gram,
                                hipFuncAttributeMaxDynamicSharedMemorySize, gst::GRAM_LDS * 8));

@@ -36,6 +36,8 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 
 constexpr int NWHITE = 20;
 constexpr int NHYPER = 10;
+constexpr int PMAX = 16;   // sampled parameters (large path; the persistent kernel takes <= 4)
+constexpr int NBMAX = 8;   // backends with their own white-noise / ECORR parameters
 __host__ __device__ constexpr int SL(int r, int s) { return r * (r + 1) / 2 + s; }
 
 // Per-chain LDS (doubles), laid out so that two chains fit per SIMD (8 per CU, 20 KB each
@@ -94,8 +96,18 @@ struct DevModel {
   int P;
   int idx_efac, idx_equad, idx_logA, idx_gamma;
   double efac_const;
-  double pmin[4], pmax[4], lp_in[4], lp_sum;
-  int hind[4], nh, wind[4], nw;
+  double pmin[PMAX], pmax[PMAX], lp_in[PMAX], lp_sum;
+  int hind[PMAX], nh, wind[PMAX], nw;
+  // general white noise (large path; the persistent kernel runs nb == 1, nec == 0):
+  // per-backend efac / log10_equad / log10_ecorr parameter indices (-1: constant / none),
+  // the backend of every TOA, and the ECORR epoch columns (internal columns
+  // ntm_pad + nf .. ntm_pad + nf + nec - 1, between the Fourier block and the residual row)
+  int nb;
+  const int* bk;            // [npad] backend of each TOA (null when nb == 1)
+  int efac_b[NBMAX], equad_b[NBMAX], ecorr_b[NBMAX];
+  int nec;
+  const int* ecb;           // [nec] backend of each ECORR column
+  double ec_count[NBMAX];   // ECORR columns per backend
   double sig_h, sig_w;
   double mh_cdf[5], mh_size[5];
   int model, vary_df, vary_alpha;
@@ -293,7 +305,7 @@ __device__ __forceinline__ double pget(const double (&x)[4], int i) {
   asm("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
   return i == 0 ? a : (i == 1 ? b : (i == 2 ? c : d));
 }
-__device__ __forceinline__ int iget4(const int (&a)[4], int i) {
+__device__ __forceinline__ int iget4(const int* a, int i) {   // a[i], i < 4
   return i == 0 ? a[0] : (i == 1 ? a[1] : (i == 2 ? a[2] : a[3]));
 }
 

@@ -128,7 +128,11 @@ __device__ __forceinline__ void mh_variate(const DevModel& md, const Rng& rng, c
     rng.uniform2(0u, tag | (uint32_t)(3 * step + 2), uidx, unused);
     int k = (int)(uidx * nind);
     k = k < nind - 1 ? k : nind - 1;
-    par = (double)(white ? iget4(md.wind, k) : iget4(md.hind, k));
+    const int* ind = white ? md.wind : md.hind;
+    int pk = ind[0];
+#pragma unroll
+    for (int j = 1; j < PMAX; ++j) pk = (k == j) ? ind[j] : pk;
+    par = (double)pk;
   }
   int cnt = 0;
 #pragma unroll
@@ -144,18 +148,62 @@ __device__ __forceinline__ void mh_variate(const DevModel& md, const Rng& rng, c
   out4[3] = exp(2.0 * delta * 2.302585092994045684);
 }
 
-__device__ __forceinline__ double lnprior4(const DevModel& md, const double (&xq)[4]) {
+typedef double XVec[PMAX];   // a chain's parameter vector (x, or an MH proposal)
+
+__device__ __forceinline__ double lnpriorP(const DevModel& md, const XVec& xq) {
   bool in = true;
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < PMAX; ++j)
     if (j < md.P) in = in && (xq[j] >= md.pmin[j]) && (xq[j] <= md.pmax[j]);
   return in ? md.lp_sum : -INFINITY;
 }
 
-__device__ __forceinline__ void load_x(const DevModel& md, const DevState& st, int c,
-                                       double (&x)[4]) {
+// x[i] for a wave-uniform or per-thread runtime index (a select chain: no scratch array)
+__device__ __forceinline__ double xget(const XVec& x, int i) {
+  double r = x[0];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) x[j] = j < md.P ? st.x[(size_t)c * md.P + j] : 0.0;
+  for (int j = 1; j < PMAX; ++j) r = (i == j) ? x[j] : r;
+  return r;
+}
+
+__device__ __forceinline__ void load_x(const DevModel& md, const DevState& st, int c,
+                                       XVec& x) {
+#pragma unroll
+  for (int j = 0; j < PMAX; ++j) x[j] = j < md.P ? st.x[(size_t)c * md.P + j] : 0.0;
+}
+
+// White-noise variances N0_t = efac_b^2 sigma_t^2 + 10^(2 equad_b) of backend b = bk[t]
+// (enterprise MeasurementNoise + EquadNoise, per selection; gibbs.py:154,268,297).  With one
+// backend this is exactly the classic model's expression.
+struct WhiteNoise {
+  double ef2[NBMAX], Q[NBMAX];
+  __device__ __forceinline__ double n0(const DevModel& md, int t) const {
+    if (md.nb <= 1) return ef2[0] * md.sig2[t] + Q[0];
+    const int b = md.bk[t];
+    double e = ef2[0], q = Q[0];
+#pragma unroll
+    for (int j = 1; j < NBMAX; ++j) {
+      e = (b == j) ? ef2[j] : e;
+      q = (b == j) ? Q[j] : q;
+    }
+    return e * md.sig2[t] + q;
+  }
+};
+
+__device__ __forceinline__ WhiteNoise white_noise(const DevModel& md, const XVec& x) {
+  WhiteNoise w;
+#pragma unroll
+  for (int b = 0; b < NBMAX; ++b) {
+    if (b < md.nb) {
+      const double ef = md.efac_b[b] >= 0 ? xget(x, md.efac_b[b]) : md.efac_const;
+      w.ef2[b] = ef * ef;
+      w.Q[b] = exp(2.0 * xget(x, md.equad_b[b]) * 2.302585092994045684);
+    } else {
+      w.ef2[b] = 0.0;
+      w.Q[b] = 0.0;
+    }
+  }
+  return w;
 }
 
 // ------------------------------------------------------------------------------------
@@ -200,9 +248,9 @@ __global__ void __launch_bounds__(TBLK) lg_white(const DevModel* __restrict__ md
   const double* yc = a.s.y + (size_t)c * a.ys;
   double* wc = a.s.w + (size_t)c * a.ys;
   double* sc = a.s.sc + (size_t)c * 16;
-  double xv[4];
+  XVec xv;
   load_x(md, a.st, c, xv);
-  if (threadIdx.x == 0) sc[SC_XLAST] = xv[md.P - 1];   // chain[ii, -1] (gibbs.py:373)
+  if (threadIdx.x == 0) sc[SC_XLAST] = xget(xv, md.P - 1);   // chain[ii, -1] (gibbs.py:373)
   const Rng rng = make_rng(a, c);
   const double* tp = tape_row(a, c);
   const bool do_white = (a.mask & 1u) || a.eval_only;
@@ -219,13 +267,14 @@ __global__ void __launch_bounds__(TBLK) lg_white(const DevModel* __restrict__ md
     la = block_sum<TBLK / 64>(la, red);
     if (!a.eval_only && threadIdx.x < NWHITE) mh_variate(md, rng, tp, threadIdx.x, mhv[threadIdx.x]);
     __syncthreads();
-    auto lnl = [&](const double (&q)[4], double Q) -> double {
-      const double ef = md.idx_efac >= 0 ? pget(q, md.idx_efac) : md.efac_const;
-      const double ef2 = ef * ef;
+    // wn.Q[0] of a one-backend model moves by 10^(2 delta) with its equad (the MH variate's
+    // 4th entry), as the persistent kernel does; with several backends every proposal's
+    // variances are recomputed from its parameters
+    auto lnl = [&](const WhiteNoise& wn) -> double {
       double sq = 0.0;
       LogProd lp;
       for (int t = threadIdx.x; t < n; t += TBLK) {
-        const double N0 = ef2 * md.sig2[t] + Q;
+        const double N0 = wn.n0(md, t);
         lp.mul(N0);
         sq += div_pos(wc[t], N0);
       }
@@ -233,42 +282,46 @@ __global__ void __launch_bounds__(TBLK) lg_white(const DevModel* __restrict__ md
       sq = block_sum<TBLK / 64>(sq, red);
       return -0.5 * ((la + sl) + sq);
     };
-    double Qx = exp(2.0 * pget(xv, md.idx_equad) * 2.302585092994045684);
-    double l0 = lnl(xv, Qx), p0 = lnprior4(md, xv);
+    WhiteNoise wx = white_noise(md, xv);
+    double l0 = lnl(wx), p0 = lnpriorP(md, xv);
     if (a.eval_only) {
       if (threadIdx.x == 0) a.out_w[c] = l0;
     } else {
       for (int step = 0; step < NWHITE; ++step) {
         const int par = (int)mhv[step][0];
-        double q[4];
+        XVec q;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) q[j] = (j == par) ? xv[j] + mhv[step][1] : xv[j];
-        const double Qq = (par == md.idx_equad) ? Qx * mhv[step][3] : Qx;
-        const double p1 = lnprior4(md, q);
+        for (int j = 0; j < PMAX; ++j) q[j] = (j == par) ? xv[j] + mhv[step][1] : xv[j];
+        WhiteNoise wq;
+        if (md.nb <= 1) {
+          wq = wx;
+          if (par == md.idx_equad) wq.Q[0] = wx.Q[0] * mhv[step][3];
+        } else {
+          wq = white_noise(md, q);
+        }
+        const double p1 = lnpriorP(md, q);
         if (p1 == -INFINITY) continue;
-        const double l1 = lnl(q, Qq);
+        const double l1 = lnl(wq);
         if ((l1 + p1) - (l0 + p0) > mhv[step][2]) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) xv[j] = q[j];
+          for (int j = 0; j < PMAX; ++j) xv[j] = q[j];
           l0 = l1;
           p0 = p1;
-          Qx = Qq;
+          wx = wq;
         }
       }
-      if (threadIdx.x < md.P) a.st.x[(size_t)c * md.P + threadIdx.x] = pget(xv, threadIdx.x);
+      if (threadIdx.x < md.P) a.st.x[(size_t)c * md.P + threadIdx.x] = xget(xv, threadIdx.x);
     }
   }
   __syncthreads();
   // N^-1, sum log N, r^T N^-1 r at the final white parameters (gibbs.py:297,309-312)
-  const double ef = md.idx_efac >= 0 ? pget(xv, md.idx_efac) : md.efac_const;
-  const double ef2 = ef * ef;
-  const double Q = exp(2.0 * pget(xv, md.idx_equad) * 2.302585092994045684);
+  const WhiteNoise wf = white_noise(md, xv);
   double sr = 0.0;
   LogProd lp;
   for (int t = threadIdx.x; t < npad; t += TBLK) {
     double wt = 0.0;
     if (t < n) {
-      const double N = (zc[t] != 0.0 ? alc[t] : 1.0) * (ef2 * md.sig2[t] + Q);
+      const double N = (zc[t] != 0.0 ? alc[t] : 1.0) * wf.n0(md, t);
       lp.mul(N);
       sr += md.resid[t] * md.resid[t] / N;
       wt = 1.0 / N;
@@ -550,8 +603,10 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
   const int c = blockIdx.x;
   const DevModel& md = mds[ds_of(a, c)];
   extern __shared__ double lsm[];
-  const int nf = md.nf, K0 = md.ntm_pad, mp = md.mp;
-  const int ms = nf + 1;               // Fourier block + augmented row
+  // the hyper-dependent columns: Fourier (power law) then ECORR epochs (10^(2 ecorr_b))
+  const int nf = md.nf + md.nec, K0 = md.ntm_pad, mp = md.mp;
+  const int nfr = md.nf;
+  const int ms = nf + 1;               // Fourier + ECORR block + augmented row
   const int SS = ms + 1;
   double* S = lsm;                     // [ms][SS]
   double* ph = S + ms * SS;            // [nf] phi^-1
@@ -565,7 +620,7 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
   const double* Gc = a.s.G + (size_t)c * mp * mp;
   const Rng rng = make_rng(a, c);
   const double* tp = tape_row(a, c);
-  double xv[4];
+  XVec xv;
   load_x(md, a.st, c, xv);
   const double logdetN = sc[SC_LOGDETN], rNr = sc[SC_RNR];
   const double ld_tm = sc[SC_LDTM], quad_tm = sc[SC_QUADTM];
@@ -575,12 +630,25 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
   if (!a.eval_only && tid < NHYPER) mh_variate(md, rng, tp, NWHITE + tid, mhv[tid]);
 
   // factor S0 + diag(phi^-1(q)) in LDS; returns the b-marginalised lnL (gibbs.py:288-329)
-  auto lnl = [&](const double (&q)[4], int& failed) -> double {
-    const double lA = pget(q, md.idx_logA);
-    const double g = pget(q, md.idx_gamma);
+  auto lnl = [&](const XVec& q, int& failed) -> double {
+    const double lA = xget(q, md.idx_logA);
+    const double g = xget(q, md.idx_gamma);
     const double lc = 2.0 * lA * 2.302585092994045684 - md.log_12pi2 + (g - 3.0) * md.log_fyr;
-    for (int f = tid; f < nf; f += LBLK) ph[f] = exp(-(lc - g * md.lfreq[f] + md.ldf[f]));
-    const double logdet_phi = ((double)nf * lc - g * md.sum_lfreq + md.sum_ldf) + md.logdet_phi_tm;
+    for (int f = tid; f < nf; f += LBLK) {
+      if (f < nfr) {
+        ph[f] = exp(-(lc - g * md.lfreq[f] + md.ldf[f]));
+      } else {
+        const int b = md.ecb[f - nfr];
+        int pi = md.ecorr_b[0];
+#pragma unroll
+        for (int j = 1; j < NBMAX; ++j) pi = (b == j) ? md.ecorr_b[j] : pi;
+        ph[f] = exp(-2.0 * xget(q, pi) * 2.302585092994045684);
+      }
+    }
+    double logdet_phi = ((double)nfr * lc - g * md.sum_lfreq + md.sum_ldf) + md.logdet_phi_tm;
+    for (int b = 0; b < md.nb; ++b)   // log 10^(2 ecorr_b) per ECORR column of backend b
+      if (md.ec_count[b] > 0.0)
+        logdet_phi += md.ec_count[b] * (2.0 * xget(q, md.ecorr_b[b]) * 2.302585092994045684);
     __syncthreads();
     for (int e = tid; e < ms * ms; e += LBLK) {
       const int i = e / ms, j = e % ms;
@@ -623,24 +691,27 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
     double l0 = 0.0, p0 = 0.0;
     const int first = ((a.mask & 2u) || a.eval_only) ? -1 : NHYPER;
     for (int step = first; step <= NHYPER; ++step) {
-      double q[4], luacc = 0.0;
+      XVec q;
+      double luacc = 0.0;
       if (step == NHYPER) {
         if (a.eval_only || !(a.mask & 4u)) break;
         redraw = true;
-        for (int j = 0; j < md.P; ++j) redraw = redraw && (xv[j] != x_last0);   // gibbs.py:373
+#pragma unroll
+        for (int j = 0; j < PMAX; ++j)
+          if (j < md.P) redraw = redraw && (xv[j] != x_last0);   // gibbs.py:373
         if (a.mask & 128u) redraw = true;
         if (!redraw || Lvalid) break;
       }
       if (step < 0 || step == NHYPER) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) q[j] = xv[j];
+        for (int j = 0; j < PMAX; ++j) q[j] = xv[j];
       } else {
         const int par = (int)mhv[step][0];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) q[j] = (j == par) ? xv[j] + mhv[step][1] : xv[j];
+        for (int j = 0; j < PMAX; ++j) q[j] = (j == par) ? xv[j] + mhv[step][1] : xv[j];
         luacc = mhv[step][2];
       }
-      const double p1 = lnprior4(md, q);
+      const double p1 = lnpriorP(md, q);
       if (step >= 0 && step < NHYPER && p1 == -INFINITY) continue;
       int f1 = 0;
       const double l1 = lnl(q, f1);
@@ -663,7 +734,7 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
       }
       if ((l1 + p1) - (l0 + p0) > luacc) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) xv[j] = q[j];
+        for (int j = 0; j < PMAX; ++j) xv[j] = q[j];
         l0 = l1;
         p0 = p1;
         Lvalid = true;
@@ -673,7 +744,7 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
     }
   }
   if (a.eval_only) return;
-  if (tid < md.P) a.st.x[(size_t)c * md.P + tid] = pget(xv, tid);
+  if (tid < md.P) a.st.x[(size_t)c * md.P + tid] = xget(xv, tid);
   if (tid == 0) {
     sc[SC_REDRAW] = redraw ? 1.0 : 0.0;
     sc[SC_FB] = (double)fb;
@@ -840,12 +911,10 @@ __global__ void __launch_bounds__(TBLK) lg_toa(const DevModel* __restrict__ mds,
   const double* yc = a.s.y + (size_t)c * a.ys;
   const Rng rng = make_rng(a, c);
   const double* tp = tape_row(a, c);
-  double xv[4];
+  XVec xv;
   load_x(md, a.st, c, xv);
   double theta = a.st.theta[c], nu = a.st.nu[c];
-  const double ef = md.idx_efac >= 0 ? pget(xv, md.idx_efac) : md.efac_const;
-  const double ef2 = ef * ef;
-  const double Q = exp(2.0 * pget(xv, md.idx_equad) * 2.302585092994045684);
+  const WhiteNoise wn = white_noise(md, xv);
   const bool mix = (md.model == 2) || (md.model == 3);
   if ((a.mask & 8u) && mix) {
     double zs = 0.0;
@@ -864,7 +933,7 @@ __global__ void __launch_bounds__(TBLK) lg_toa(const DevModel* __restrict__ mds,
   if ((a.mask & 16u) && mix) {
     const double SQ2PI = 2.5066282746310002;  // np.sqrt(2*np.pi)
     for (int t = tid; t < n; t += TBLK) {
-      const double N0 = ef2 * md.sig2[t] + Q;
+      const double N0 = wn.n0(md, t);
       const double Nv = alc[t] * N0;
       const double y = yc[t];
       const double sd1 = sqrt(Nv);
@@ -896,7 +965,7 @@ __global__ void __launch_bounds__(TBLK) lg_toa(const DevModel* __restrict__ mds,
     if (zs >= 1.0) {
       for (int t = tid; t < n; t += TBLK) {
         const double zf = zc[t] != 0.0 ? 1.0 : 0.0;
-        const double N0 = ef2 * md.sig2[t] + Q;
+        const double N0 = wn.n0(md, t);
         const double top = ((yc[t] * yc[t]) * zf / N0 + nu) / 2.0;
         const double G = tp ? tp[TP_DELTA + m + 1 + nst + t]
                             : gamma_mt((zf + nu) / 2.0, rng, (uint32_t)t, TAG_ALPHA);

@@ -198,5 +198,46 @@ def scaled_synthetic(n: int = 100_000, components: int = 60, ntm: int = 300, see
                       meta={"z_true": z, "seed": seed, "theta": theta})
 
 
-__all__ = ["load_j1713_raw", "scaled_synthetic", "design_matrix", "simulate_residuals", "j1713",
+def multiband(nepochs: int = 60, nsub: int = 3, backends=("ASP", "GUPPI"), seed: int = 1643,
+              theta: float = 0.05, sigma_out: float = 1e-6, efac=(1.1, 0.9),
+              log10_equad=(-6.6, -7.0), log10_ecorr=(-6.5, -6.8), log10_A: float = -14.0,
+              gamma: float = 4.33, components: int = 10) -> PulsarData:
+    """A NANOGrav-style multi-backend, multi-band dataset for the general white-noise model
+    of the notebook's J1643-1224 run (gibbs_likelihood.ipynb cell 2: efac, equad, ECORR per
+    backend, power-law red noise, timing model) -- not in the reference's data, built with
+    the simulate_data.py recipe on the first ``nepochs`` J1713+0747 epochs:
+
+    each epoch has ``nsub`` sub-band TOAs at the same arrival time (0.1 s apart, one ECORR
+    epoch), the first half of the epochs on ``backends[0]``, the rest on ``backends[1]``;
+    white noise ``efac_b sigma`` + ``10^equad_b`` per TOA, ECORR jitter ``10^ecorr_b`` shared
+    by an epoch's TOAs, power-law red noise, Bernoulli(theta) outliers, and the timing model
+    projected out.  The per-backend true values are in ``meta``."""
+    raw = load_j1713_raw()
+    mjd0 = (raw["mjd_int"].astype(np.float64) + raw["mjd_frac"])[:nepochs]
+    rng = np.random.default_rng(seed)
+    mjd = np.repeat(mjd0, nsub) + np.tile(np.arange(nsub) * 0.1 / DAY_SEC, nepochs)
+    toas = mjd * DAY_SEC
+    n = len(toas)
+    ep = np.repeat(np.arange(nepochs), nsub)
+    bk = (ep >= nepochs // 2).astype(np.int64)
+    labels = np.array(backends)[bk]
+    err = 10 ** (-7 + rng.standard_normal(n) * 0.2)
+    M = design_matrix(mjd, raw["par"], raw["fit"])
+    U = np.linalg.svd(M, full_matrices=False)[0]
+    F, ff = fourier_basis(toas, components)
+    red = F @ (np.sqrt(powerlaw(ff, log10_A, gamma)) * rng.standard_normal(2 * components))
+    ef, eq, ec = (np.asarray(v, dtype=np.float64)[bk] for v in (efac, log10_equad, log10_ecorr))
+    jitter = (10 ** np.asarray(log10_ecorr)[(np.arange(nepochs) >= nepochs // 2).astype(int)]
+              * rng.standard_normal(nepochs))[ep]
+    white = np.sqrt((ef * err) ** 2 + 10 ** (2 * eq)) * rng.standard_normal(n)
+    z = (rng.random(n) < theta).astype(np.int64)
+    r = red + jitter + np.where(z == 1, sigma_out * rng.standard_normal(n), white)
+    r = r - U @ (U.T @ r)
+    return PulsarData(name="MB", toas=toas, residuals=r, toaerrs=err, Mmat=M, backends=labels,
+                      meta={"z_true": z, "seed": seed, "theta": theta, "efac": efac,
+                            "log10_equad": log10_equad, "log10_ecorr": log10_ecorr,
+                            "epoch": ep})
+
+
+__all__ = ["load_j1713_raw", "multiband", "scaled_synthetic", "design_matrix", "simulate_residuals", "j1713",
            "at_epochs", "load_partim", "simulate_data", "FYR"]

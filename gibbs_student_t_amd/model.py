@@ -20,14 +20,27 @@ this module restates the *specific* model `run_sims.py:57-83` builds:
 * timing model: ``BasisGP`` on the SVD basis ``U`` of the design matrix with prior weight
   ``1e40`` (run_sims.py:22-29,69-71).
 
+and, as the notebook's J1643-1224 model uses them (gibbs_likelihood.ipynb cell 2), the
+general white-noise options the reference sampler handles through its index sets
+(gibbs.py:64-77: any ``ecorr`` parameter is a hyper parameter, any ``efac``/``equad`` a white
+one):
+
+* ``selection="backend"``: one efac / log10_equad (/ log10_ecorr) per backend
+  (enterprise ``selections.by_backend``), parameters named ``{psr}_{backend}_efac`` etc.;
+  ``"none"`` (``no_selection``): one set named ``{psr}_efac`` etc.
+* ``log10_ecorr=(pmin, pmax)``: ECORR as a basis GP (enterprise ``EcorrBasisModel``): one
+  column per observing epoch with at least two TOAs (``quantization_matrix``), per backend
+  under ``selection="backend"``, prior variance ``10^(2 log10_ecorr)``.
+
 The enterprise formulas (Fourier design matrix, power law, ``phiinv``/``logdet`` from a
 diagonal ``phi``) are restated from their published form; parity against enterprise
 itself is **unpinned** (no fixture of it exists in the reference).  Everything else in the
 build -- the CPU oracle, the golden generator and the HIP path -- consumes this one model,
 so the sampler parity is exact with respect to it.
 
-Column order of the basis ``T`` is ``[Fourier (2*components) | timing model]`` as in
-enterprise's signal-collection order ``ef + eq + rn + tm`` (run_sims.py:74).
+Column order of the basis ``T`` is ``[Fourier (2*components) | timing model | ECORR]`` as in
+enterprise's signal-collection order ``ef + eq + rn + tm (+ ec)`` (run_sims.py:74,
+gibbs_likelihood.ipynb cell 2).
 """
 from __future__ import annotations
 
@@ -101,6 +114,28 @@ def powerlaw(f: np.ndarray, log10_A: float, gamma: float, components: int = 2):
             * f ** (-gamma) * np.repeat(df, components))
 
 
+def quantization_matrix(toas: np.ndarray, dt: float = 1.0, nmin: int = 2):
+    """Epoch basis of ECORR (enterprise ``utils.create_quantization_matrix``): TOAs sorted
+    by time, a new epoch whenever a TOA is ``dt`` seconds or more after the epoch's first
+    TOA; epochs with fewer than ``nmin`` TOAs get no column.  Returns ``U`` (n x epochs,
+    one 1 per row of a TOA in a kept epoch)."""
+    toas = np.asarray(toas, dtype=np.float64)
+    isort = np.argsort(toas, kind="stable")
+    buckets = [[isort[0]]] if len(toas) else []
+    ref = toas[isort[0]] if len(toas) else 0.0
+    for i in isort[1:]:
+        if toas[i] - ref < dt:
+            buckets[-1].append(i)
+        else:
+            buckets.append([i])
+            ref = toas[i]
+    buckets = [b for b in buckets if len(b) >= nmin]
+    U = np.zeros((len(toas), len(buckets)))
+    for e, b in enumerate(buckets):
+        U[b, e] = 1.0
+    return U
+
+
 def svd_tm_basis(Mmat: np.ndarray):
     """Timing-model basis: left singular vectors of the design matrix (run_sims.py:22-25)."""
     u, s, _ = np.linalg.svd(Mmat, full_matrices=False)
@@ -118,6 +153,7 @@ class PulsarData:
     Mmat: np.ndarray        # timing-model design matrix (n x ntm)
     freqs: np.ndarray | None = None
     meta: dict = field(default_factory=dict)
+    backends: np.ndarray | None = None   # backend label of each TOA (tim-file flag -be/-f)
 
     @property
     def n(self):
@@ -133,30 +169,72 @@ class PTA:
 
     def __init__(self, psr: PulsarData, components: int = 30, efac=1.0,
                  log10_equad=(-10.0, -5.0), log10_A=(-18.0, -12.0), gamma=(1.0, 7.0),
-                 tm_weight: float = 1e40, Tspan: float | None = None):
+                 tm_weight: float = 1e40, Tspan: float | None = None, *,
+                 selection: str = "none", log10_ecorr=None, ecorr_dt: float = 1.0):
         self.psr = psr
         self.components = int(components)
         self._r = np.asarray(psr.residuals, dtype=np.float64)
         self._toaerrs = np.asarray(psr.toaerrs, dtype=np.float64)
-        self.F, self.Ffreqs = fourier_basis(np.asarray(psr.toas, dtype=np.float64),
-                                            self.components, Tspan)
+        toas = np.asarray(psr.toas, dtype=np.float64)
+        self.F, self.Ffreqs = fourier_basis(toas, self.components, Tspan)
         U, w = svd_tm_basis(np.asarray(psr.Mmat, dtype=np.float64))
         self.U = U
         self.tm_phi = w * tm_weight          # tm_prior (run_sims.py:27-29)
         self.tm_weight = float(tm_weight)
-        self.T = np.hstack([self.F, self.U])
-        nm = psr.name
+        self._set_backends(psr.backends, selection)
+        cols, self.ecorr_backend = [], np.zeros(0, dtype=np.int64)
+        if log10_ecorr is not None:
+            # one quantization per backend (enterprise applies the basis per selection mask)
+            eb = []
+            for b in range(len(self.backend_names)):
+                mask = self.bidx == b
+                Ub = quantization_matrix(toas[mask], ecorr_dt)
+                full = np.zeros((len(toas), Ub.shape[1]))
+                full[mask] = Ub
+                cols.append(full)
+                eb += [b] * Ub.shape[1]
+            self.ecorr_backend = np.array(eb, dtype=np.int64)
+        self.Uec = np.hstack(cols) if cols else np.zeros((len(toas), 0))
+        self.T = np.hstack([self.F, self.U, self.Uec])
+        self._build_params(efac, log10_equad, log10_A, gamma, log10_ecorr)
+
+    # --- white-noise structure ----------------------------------------------------------
+    def _set_backends(self, backends, selection):
+        if selection not in ("none", "backend"):
+            raise ValueError("selection must be 'none' or 'backend'")
+        n = len(self._r)
+        self.selection = selection
+        if selection == "backend":
+            if backends is None:
+                raise ValueError("selection='backend' needs psr.backends")
+            labels = np.asarray(backends).astype(str)
+            self.backend_names = sorted(set(labels.tolist()))
+            self.bidx = np.array([self.backend_names.index(v) for v in labels], dtype=np.int64)
+        else:
+            self.backend_names = [""]
+            self.bidx = np.zeros(n, dtype=np.int64)
+
+    def _pname(self, b, what):
+        be = self.backend_names[b]
+        return f"{self.psr.name}_{be}_{what}" if be else f"{self.psr.name}_{what}"
+
+    def _build_params(self, efac, log10_equad, log10_A, gamma, log10_ecorr):
+        nm = self.psr.name
         plist = []
+        nb = len(self.backend_names)
         if isinstance(efac, (tuple, list)):
-            plist.append(Uniform(f"{nm}_efac", *efac))
+            plist += [Uniform(self._pname(b, "efac"), *efac) for b in range(nb)]
             self.efac_const = None
         else:
             self.efac_const = float(efac)
-        plist.append(Uniform(f"{nm}_log10_equad", *log10_equad))
+        plist += [Uniform(self._pname(b, "log10_equad"), *log10_equad) for b in range(nb)]
+        if log10_ecorr is not None:
+            plist += [Uniform(self._pname(b, "log10_ecorr"), *log10_ecorr) for b in range(nb)]
         plist.append(Uniform(f"{nm}_log10_A", *log10_A))
         plist.append(Uniform(f"{nm}_gamma", *gamma))
         # enterprise returns params sorted by name
         self._params = sorted(plist, key=lambda p: p.name)
+        self.has_ecorr = log10_ecorr is not None
 
     @classmethod
     def from_arrays(cls, name, residuals, toaerrs, T, Ffreqs, components, tm_weight=1e40,
@@ -174,18 +252,20 @@ class PTA:
         obj.F, obj.Ffreqs = T[:, :nf], np.asarray(Ffreqs, dtype=np.float64)
         obj.U = T[:, nf:]
         obj.tm_weight = float(tm_weight)
+        n_ec = int(priors.pop("n_ecorr", 0))
+        ntm = T.shape[1] - nf - n_ec
+        obj.U = T[:, nf:nf + ntm]
+        obj.Uec = T[:, nf + ntm:]
         obj.tm_phi = np.ones(obj.U.shape[1]) * obj.tm_weight
         obj.T = T
-        plist = []
-        if isinstance(efac, (tuple, list)):
-            plist.append(Uniform(f"{name}_efac", *efac))
-            obj.efac_const = None
-        else:
-            obj.efac_const = float(efac)
-        plist.append(Uniform(f"{name}_log10_equad", *priors.get("log10_equad", (-10., -5.))))
-        plist.append(Uniform(f"{name}_log10_A", *priors.get("log10_A", (-18., -12.))))
-        plist.append(Uniform(f"{name}_gamma", *priors.get("gamma", (1., 7.))))
-        obj._params = sorted(plist, key=lambda p: p.name)
+        obj.psr.backends = priors.pop("backends", None)
+        obj._set_backends(obj.psr.backends, priors.pop("selection", "none"))
+        eb = priors.pop("ecorr_backend", None)
+        obj.ecorr_backend = (np.zeros(0, dtype=np.int64) if eb is None
+                             else np.asarray(eb, dtype=np.int64))
+        obj._build_params(efac, priors.get("log10_equad", (-10., -5.)),
+                          priors.get("log10_A", (-18., -12.)), priors.get("gamma", (1., 7.)),
+                          priors.get("log10_ecorr"))
         return obj
 
     # --- the protocol ---------------------------------------------------------------
@@ -207,14 +287,26 @@ class PTA:
         return params[f"{self.psr.name}_{suffix}"]
 
     def get_ndiag(self, params):
-        efac = self.efac_const if self.efac_const is not None else self._value(params, "efac")
-        eq = self._value(params, "log10_equad")
-        return [efac ** 2 * self._toaerrs ** 2 + 10 ** (2 * eq) * np.ones(len(self._r))]
+        if len(self.backend_names) == 1:
+            efac = (self.efac_const if self.efac_const is not None
+                    else params[self._pname(0, "efac")])
+            eq = params[self._pname(0, "log10_equad")]
+            return [efac ** 2 * self._toaerrs ** 2 + 10 ** (2 * eq) * np.ones(len(self._r))]
+        nb = len(self.backend_names)
+        efac = np.array([self.efac_const if self.efac_const is not None
+                         else params[self._pname(b, "efac")] for b in range(nb)])[self.bidx]
+        eq = np.array([params[self._pname(b, "log10_equad")] for b in range(nb)])[self.bidx]
+        return [efac ** 2 * self._toaerrs ** 2 + 10 ** (2 * eq)]
 
     def get_phi(self, params):
         pl = powerlaw(self.Ffreqs, self._value(params, "log10_A"),
                       self._value(params, "gamma"), components=2)
-        return [np.concatenate([pl, self.tm_phi])]
+        parts = [pl, self.tm_phi]
+        if self.n_ecorr:
+            ec = np.array([params[self._pname(b, "log10_ecorr")]
+                           for b in range(len(self.backend_names))])
+            parts.append(10 ** (2 * ec[self.ecorr_backend]))
+        return [np.concatenate(parts)]
 
     def get_phiinv(self, params, logdet=False):
         phi = self.get_phi(params)[0]
@@ -238,6 +330,20 @@ class PTA:
     @property
     def ntm(self):
         return self.U.shape[1]
+
+    @property
+    def n_ecorr(self):
+        return self.Uec.shape[1]
+
+    @property
+    def nbackend(self):
+        return len(self.backend_names)
+
+    def backend_param_indices(self, what):
+        """Index into ``params`` of each backend's ``what`` parameter (-1: none / constant)."""
+        names = self.param_names
+        return np.array([names.index(self._pname(b, what)) if self._pname(b, what) in names
+                         else -1 for b in range(len(self.backend_names))], dtype=np.int64)
 
     def param_index(self, suffix):
         for i, p in enumerate(self._params):
@@ -277,5 +383,5 @@ def mh_constants():
 
 
 __all__ = ["Constant", "Uniform", "PulsarData", "PTA", "fourier_basis", "powerlaw",
-           "svd_tm_basis", "df_tables", "hyper_white_indices", "mh_constants",
+           "svd_tm_basis", "quantization_matrix", "df_tables", "hyper_white_indices", "mh_constants",
            "FYR", "YR_SEC", "DAY_SEC"]

@@ -53,6 +53,16 @@ def model_desc(pta, cfg: dict):
         "A": np.ascontiguousarray(A, dtype=np.float64),
         "B": np.ascontiguousarray(B, dtype=np.float64),
     }
+    # general white noise (ABI 3): per-backend parameters and ECORR basis columns
+    nb = int(getattr(pta, "nbackend", 1))
+    n_ec = int(getattr(pta, "n_ecorr", 0))
+    if nb > 1 or n_ec:
+        keep.update(
+            bk=np.ascontiguousarray(pta.bidx, dtype=np.int32),
+            efi=np.ascontiguousarray(pta.backend_param_indices("efac"), dtype=np.int32),
+            eqi=np.ascontiguousarray(pta.backend_param_indices("log10_equad"), dtype=np.int32),
+            eci=np.ascontiguousarray(pta.backend_param_indices("log10_ecorr"), dtype=np.int32),
+            ecb=np.ascontiguousarray(pta.ecorr_backend, dtype=np.int32))
     dp = lambda a: a.ctypes.data_as(_abi._D)  # noqa: E731
     ip = lambda a: a.ctypes.data_as(_abi._I)  # noqa: E731
     model = cfg.get("model", "gaussian")
@@ -77,6 +87,14 @@ def model_desc(pta, cfg: dict):
         pspin=float(cfg.get("pspin") or 0.0),
         df_A=dp(keep["A"]), df_B=dp(keep["B"]),
     )
+    if nb > 1 or n_ec:
+        desc.nbackend = nb
+        desc.backend = ip(keep["bk"])
+        desc.efac_idx = ip(keep["efi"])
+        desc.equad_idx = ip(keep["eqi"])
+        desc.ecorr_idx = ip(keep["eci"])
+        desc.n_ecorr = n_ec
+        desc.ecorr_backend = ip(keep["ecb"]) if n_ec else None
     return desc, keep
 
 

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GST_ABI_VERSION 2
+#define GST_ABI_VERSION 3
 
 /* Outlier model kind: Gibbs(model=...) (gibbs.py:9,32,187-226). */
 enum gst_outlier_model {
@@ -92,6 +92,21 @@ typedef struct gst_model_desc {
   double pspin;            /* vvh17 only */
   const double* df_A;      /* 30: n*(nu/2)*log(nu/2) for nu=1..30 (gibbs.py:333-334) */
   const double* df_B;      /* 30: n*gammaln(nu/2) */
+  /* General white noise (ABI 3; all zero / NULL = the classic single-backend model above).
+   * The reference treats any efac / equad parameter as white and any ecorr parameter as
+   * hyper (gibbs.py:64-77), e.g. the notebook's J1643-1224 model (efac, equad and an ECORR
+   * basis, gibbs_likelihood.ipynb cell 2) or per-backend selections.  Such models run on
+   * the large path (GST_PATH_LARGE; AUTO picks it); nparams may then be up to 16. */
+  int nbackend;            /* backends with their own parameters, 1..8 (0 = 1) */
+  const int* backend;      /* n: backend of each TOA (NULL: all 0) */
+  const int* efac_idx;     /* nbackend: parameter index of each backend's efac, -1 =
+                              efac_const (NULL: idx_efac for every backend) */
+  const int* equad_idx;    /* nbackend: each backend's log10_equad (NULL: idx_equad) */
+  const int* ecorr_idx;    /* nbackend: each backend's log10_ecorr, -1 = none (NULL: none) */
+  int n_ecorr;             /* ECORR basis columns: the LAST n_ecorr columns of T, prior
+                              variance 10^(2 log10_ecorr) of their backend; m = nfourier +
+                              ntm + n_ecorr */
+  const int* ecorr_backend;/* n_ecorr: backend of each ECORR column */
 } gst_model_desc;
 
 /* Per-chain state, device pointers, chain-major.  x[C*P], b[C*m], z/alpha/pout[C*nmax]

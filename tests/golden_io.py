@@ -12,7 +12,7 @@ from gibbs_student_t_amd.model import PTA
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 # fixture-name prefix -> tests/golden/{prefix}_dataset.npz (tools/gen_golden.py)
-DATASETS = ("sim", "twob", "simclean", "scaled", "c3", "c4t", "c20", "tm22")
+DATASETS = ("sim", "twob", "simclean", "scaled", "c3", "c4t", "c20", "tm22", "mb", "mbn")
 
 CHAIN_KEYS = ("chain", "bchain", "zchain", "poutchain", "thetachain", "alphachain", "dfchain")
 
@@ -24,6 +24,14 @@ def fixture_names():
 def load_dataset(efac=False, dataset="j1713"):
     fn = "j1713_dataset_efac.npz" if efac else f"{dataset}_dataset.npz"
     d = np.load(os.path.join(GOLDEN, fn), allow_pickle=False)
+    if "backends" in d.files:     # general white-noise model (tools/gen_golden.py general)
+        name = str(d["names"][0]).split("_")[0]
+        return PTA.from_arrays(name, d["residuals"], d["toaerrs"], d["T"], d["Ffreqs"],
+                               int(d["components"]), float(d["tm_weight"]),
+                               efac=(0.2, 10.0) if int(d["efac_varied"]) else 1.0,
+                               backends=d["backends"], selection=str(d["selection"]),
+                               n_ecorr=int(d["n_ecorr"]), ecorr_backend=d["ecorr_backend"],
+                               log10_ecorr=tuple(d["log10_ecorr"]))
     return PTA.from_arrays("J1713+0747", d["residuals"], d["toaerrs"], d["T"], d["Ffreqs"],
                            int(d["components"]), float(d["tm_weight"]),
                            efac=(0.2, 10.0) if efac else 1.0)

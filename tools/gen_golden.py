@@ -280,9 +280,16 @@ def run_one(pta, name, kw, seed, niter, x0=None):
 
 
 def dataset_arrays(pta, psr):
-    return dict(toas=psr.toas, residuals=psr.residuals, toaerrs=psr.toaerrs, Mmat=psr.Mmat,
-                T=pta.T, Ffreqs=pta.Ffreqs, components=pta.components,
-                tm_weight=pta.tm_weight, names=np.array(pta.param_names))
+    out = dict(toas=psr.toas, residuals=psr.residuals, toaerrs=psr.toaerrs, Mmat=psr.Mmat,
+               T=pta.T, Ffreqs=pta.Ffreqs, components=pta.components,
+               tm_weight=pta.tm_weight, names=np.array(pta.param_names))
+    if pta.nbackend > 1 or pta.n_ecorr or getattr(pta, "has_ecorr", False):
+        # general white-noise model (per-backend parameters, ECORR basis columns)
+        out.update(backends=np.asarray(psr.backends).astype(str), selection=pta.selection,
+                   n_ecorr=pta.n_ecorr, ecorr_backend=pta.ecorr_backend,
+                   efac_varied=int(pta.efac_const is None),
+                   log10_ecorr=np.array([-8.5, -5.0]))
+    return out
 
 
 def simclean(niter=12):
@@ -374,8 +381,41 @@ def shapes(niter=12):
                   file=sys.stderr)
 
 
+def general(niter=12):
+    """The general white-noise model of the notebook's J1643-1224 run (gibbs_likelihood.ipynb
+    cell 2: efac, equad, ECORR basis, power-law red noise, timing model) on a multi-band,
+    two-backend dataset (gdata.multiband: 60 J1713 epochs x 3 sub-band TOAs, ASP then GUPPI):
+
+    * ``mb``: ``selection="backend"``, varied efac, equad and ECORR per backend: P = 8
+      (white index set of 4, hyper set of 4: the two ecorr, log10_A, gamma, gibbs.py:64-77),
+      10 red-noise components, 60 ECORR epoch columns (m = 94);
+    * ``mbn``: ``no_selection`` as the notebook runs it: P = 5 (efac, ecorr, equad, gamma,
+      log10_A), one ECORR prior for all 60 epochs.
+    """
+    psr = gdata.multiband()
+    pta_b = PTA(psr, components=10, efac=(0.2, 10.0), selection="backend",
+                log10_ecorr=(-8.5, -5.0))
+    pta_n = PTA(psr, components=10, efac=(0.2, 10.0), log10_ecorr=(-8.5, -5.0))
+    x0b = [1.1, -6.5, -6.6, 0.9, -6.8, -7.0, 4.33, -14.0]
+    x0n = [1.0, 4.33, -14.0, -6.6, -6.8]    # efac, gamma, log10_A, log10_ecorr, log10_equad
+    for tag, pta_g, x0, models in (("mb", pta_b, x0b, ("beta", "t", "gaussian")),
+                                   ("mbn", pta_n, x0n, ("beta", "vvh17"))):
+        np.savez_compressed(os.path.join(OUTDIR, f"{tag}_dataset.npz"),
+                            **dataset_arrays(pta_g, psr))
+        for j, name in enumerate(models):
+            out = run_one(pta_g, name, MODELS[name], seed=7300 + 13 * j + len(tag),
+                          niter=niter, x0=x0)
+            out["model_kw"] = np.array(repr(MODELS[name]))
+            np.savez_compressed(os.path.join(OUTDIR, f"ref_{tag}_{name}_fixed.npz"), **out)
+            print(tag, name, "P", len(x0), "m", pta_g.m, "cond:",
+                  np.nanmax(out["tape_b_cond"]), file=sys.stderr)
+
+
 def main():
     os.makedirs(OUTDIR, exist_ok=True)
+    if "--only-general" in sys.argv:
+        general(12)
+        return
     if "--only-shapes" in sys.argv:
         shapes(12)
         return
@@ -433,6 +473,7 @@ def main():
     scaled()
     configs34(niter)
     shapes(niter)
+    general(niter)
 
 
 if __name__ == "__main__":
