@@ -447,7 +447,8 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
   const int MT = sh ? sh->MT : 0, K0 = sh ? sh->K0 : 0;
   const int raug = sh ? sh->RA : 0;
   const int nsl = (nmax + 63) / 64;
-  const int NS = nsl <= 2 ? 2 : (nsl <= 3 ? 3 : 4);
+  // TOA slots of 64 held in registers: 2, 3, 4 (J1713-sized), 6, 8 (mid-size, n <= 512)
+  const int NS = nsl <= 2 ? 2 : (nsl <= 3 ? 3 : (nsl <= 4 ? 4 : (nsl <= 6 ? 6 : 8)));
   const bool fits = sh && classic(d) && round_up(nmax, 4) <= 64 * NS &&
                     pick(MT, NS, K0, raug, false, 4, false);
   int path = cx->path_req;

@@ -20,12 +20,18 @@ typedef void (*kfn_t)(const DevModel*, const DevState, const DevRec, const DevTa
   X(10, 2, 2, 76) /* J1713-like, n <= 128 (no_outlier datasets) */                 \
   X(10, 3, 2, 76) /* J1713+0747: n = 130, 30 red-noise components, 14 TM columns */ \
   X(10, 4, 2, 76) /* n <= 256 */                                                   \
+  X(10, 6, 2, 76) /* mid-size pulsars: n <= 384 */                                 \
+  X(10, 8, 2, 76) /* n <= 512 */                                                   \
   X(8, 2, 2, 56)  /* <= 20 red-noise components, <= 16 TM columns */               \
   X(8, 3, 2, 56)                                                                   \
   X(8, 4, 2, 56)                                                                   \
+  X(8, 6, 2, 56)                                                                   \
+  X(8, 8, 2, 56)                                                                   \
   X(10, 2, 3, 76) /* <= 26 components with 17..24 TM columns */                    \
   X(10, 3, 3, 76)                                                                  \
-  X(10, 4, 3, 76)
+  X(10, 4, 3, 76)                                                                  \
+  X(10, 6, 3, 76)                                                                  \
+  X(10, 8, 3, 76)
 
 // tape: parity mode (4 chains per workgroup); wpb: chains per workgroup (4, or 2 / 1 for
 // sampling launches with fewer chains than fill every SIMD); occ2: the two-chains-per-SIMD

@@ -200,7 +200,7 @@ int gst_eval_lnlike(void* ctx, const gst_state* state, int nchains, double* out_
 int gst_sync(void* ctx, void* stream);
 
 /* Execution path.  The persistent path keeps a whole chain in one wavefront for all of a
- * launch's sweeps (n <= 256 and up to 30 red-noise components with <= 16 timing-model
+ * launch's sweeps (n <= 512 and up to 30 red-noise components with <= 16 timing-model
  * columns, 26 with <= 24; smaller models run padded with unit-prior dummy columns); the
  * large path runs
  * each sweep as a pipeline of kernels (fp64-MFMA Gram shared by all chains, blocked

@@ -55,3 +55,32 @@ def test_simulate_data_pair():
     assert out.n == 130 and clean.n == 130 - z.sum()
     pta = model.PTA(clean)
     assert pta.T.shape[0] == clean.n
+
+
+def test_general_white_noise_model():
+    """Per-backend efac / equad / ECORR (the notebook's J1643-1224 model, with
+    enterprise's by_backend selection): parameter names sorted as enterprise sorts them,
+    N0 per TOA from its backend's parameters, ECORR columns = observing epochs with >= 2
+    TOAs, each with prior variance 10^(2 log10_ecorr) of its backend."""
+    psr = data.multiband(nepochs=20, nsub=3)
+    pta = model.PTA(psr, components=10, efac=(0.2, 10.0), selection="backend",
+                    log10_ecorr=(-8.5, -5.0))
+    assert pta.param_names == sorted(pta.param_names) and len(pta.params) == 8
+    assert pta.n_ecorr == 20 and pta.nbackend == 2 and pta.m == 20 + pta.ntm + 20
+    U = pta.T[:, -20:]
+    assert np.all(U.sum(axis=0) == 3) and np.all(U.sum(axis=1) == 1)   # one epoch per TOA
+    x = {p.name: v for p, v in zip(pta.params, [1.5, -6.0, -6.5, 0.8, -7.0, -7.5, 4.0, -14.0])}
+    n0 = pta.get_ndiag(x)[0]
+    bk = pta.bidx
+    ef = np.where(bk == 0, 1.5, 0.8)
+    eq = np.where(bk == 0, -6.5, -7.5)
+    np.testing.assert_array_equal(n0, ef ** 2 * pta._toaerrs ** 2 + 10 ** (2 * eq))
+    phi = pta.get_phi(x)[0][-20:]
+    np.testing.assert_array_equal(phi, 10 ** (2 * np.where(pta.ecorr_backend == 0, -6.0, -7.0)))
+    hind, wind = model.hyper_white_indices(pta.param_names)
+    assert [pta.param_names[i] for i in hind] == ["MB_ASP_log10_ecorr", "MB_GUPPI_log10_ecorr",
+                                                  "MB_gamma", "MB_log10_A"]
+    assert len(wind) == 4
+    # quantization: TOAs within 1 s share an epoch, epochs with one TOA get no column
+    q = model.quantization_matrix(np.array([0.0, 0.5, 10.0, 20.0, 20.2]))
+    np.testing.assert_array_equal(q, [[1, 0], [1, 0], [0, 0], [0, 1], [0, 1]])

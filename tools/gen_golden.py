@@ -411,10 +411,28 @@ def general(niter=12):
                   np.nanmax(out["tape_b_cond"]), file=sys.stderr)
 
 
+def mid(niter=12):
+    """A mid-size pulsar for the register-resident kernel's wide TOA instances (NS = 6, 8
+    slots of 64 TOAs): 130 J1713+0747 epochs x 3 sub-band TOAs (gdata.multiband, one
+    backend's labels ignored), n = 390, the classic run_sims model (30 components)."""
+    psr = gdata.multiband(nepochs=130, nsub=3, seed=390)
+    pta_m = PTA(psr)
+    np.savez_compressed(os.path.join(OUTDIR, "mid_dataset.npz"), **dataset_arrays(pta_m, psr))
+    for j, name in enumerate(("beta", "t")):
+        out = run_one(pta_m, name, MODELS[name], seed=8100 + 11 * j, niter=niter,
+                      x0=[4.33, -14.0, -7.6])
+        out["model_kw"] = np.array(repr(MODELS[name]))
+        np.savez_compressed(os.path.join(OUTDIR, f"ref_mid_{name}_fixed.npz"), **out)
+        print("mid", name, "n", pta_m.n, "cond:", np.nanmax(out["tape_b_cond"]), file=sys.stderr)
+
+
 def main():
     os.makedirs(OUTDIR, exist_ok=True)
     if "--only-general" in sys.argv:
         general(12)
+        return
+    if "--only-mid" in sys.argv:
+        mid(12)
         return
     if "--only-shapes" in sys.argv:
         shapes(12)
@@ -474,6 +492,7 @@ def main():
     configs34(niter)
     shapes(niter)
     general(niter)
+    mid(niter)
 
 
 if __name__ == "__main__":

@@ -8,4 +8,5 @@ step 900 $O/gpu_tests.txt $PYT -m gpu tests/
 step 600 $O/bitwise2048.txt python -u tools/ab_bitwise.py gibbs_student_t_amd/libgst_base.so gibbs_student_t_amd/libgst.so 2048 60
 step 600 $O/ab.txt bash tools/ab_bench.sh gibbs_student_t_amd/libgst_base.so gibbs_student_t_amd/libgst.so
 cat $O/ab.txt
+step 300 $O/mid_size.txt python -u tools/mid_size.py 2048 100 $O/mid_size.json
 bash tools/profile_r3.sh
