@@ -669,8 +669,10 @@ static int launch(Ctx* cx, const gst_state* s, const gst_records* r, const gst_t
   const dim3 grid(pair ? C : (C + wpb - 1) / wpb), block(pair ? 128 : 64 * wpb);
   // two chains per SIMD: the progress rule of fair_prio (with more chains than resident
   // slots, the later workgroups count as behind and the launch's tail shortens: config 4
-  // 8.24 -> 8.32 M chain-sweeps/s)
-  if (!tape && !pair && C > 4 * cx->ncu) {
+  // 8.24 -> 8.32 M chain-sweeps/s).  Only in launches that run the red-noise block: the
+  // counter's same-address atomics serialise at ~12 ns each across the XCDs, which a full
+  // sweep hides but a stage-masked launch of a few microseconds per sweep would be timing
+  if (!tape && !pair && C > 4 * cx->ncu && (mask & GST_STAGE_HYPER)) {
     HIP_OK(hipMemsetAsync(cx->prog, 0, sizeof(unsigned long long), st));
     ds.prog = cx->prog;
   }

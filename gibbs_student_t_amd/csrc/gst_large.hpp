@@ -267,9 +267,9 @@ __global__ void __launch_bounds__(TBLK) lg_white(const DevModel* __restrict__ md
     la = block_sum<TBLK / 64>(la, red);
     if (!a.eval_only && threadIdx.x < NWHITE) mh_variate(md, rng, tp, threadIdx.x, mhv[threadIdx.x]);
     __syncthreads();
-    // wn.Q[0] of a one-backend model moves by 10^(2 delta) with its equad (the MH variate's
-    // 4th entry), as the persistent kernel does; with several backends every proposal's
-    // variances are recomputed from its parameters
+    // a proposal's variances come from its parameters, except that Q of a one-backend model
+    // moves by 10^(2 delta) with its equad (the MH variate's 4th entry), as the persistent
+    // kernel carries it
     auto lnl = [&](const WhiteNoise& wn) -> double {
       double sq = 0.0;
       LogProd lp;
@@ -292,13 +292,8 @@ __global__ void __launch_bounds__(TBLK) lg_white(const DevModel* __restrict__ md
         XVec q;
 #pragma unroll
         for (int j = 0; j < PMAX; ++j) q[j] = (j == par) ? xv[j] + mhv[step][1] : xv[j];
-        WhiteNoise wq;
-        if (md.nb <= 1) {
-          wq = wx;
-          if (par == md.idx_equad) wq.Q[0] = wx.Q[0] * mhv[step][3];
-        } else {
-          wq = white_noise(md, q);
-        }
+        WhiteNoise wq = white_noise(md, q);
+        if (md.nb <= 1) wq.Q[0] = (par == md.idx_equad) ? wx.Q[0] * mhv[step][3] : wx.Q[0];
         const double p1 = lnpriorP(md, q);
         if (p1 == -INFINITY) continue;
         const double l1 = lnl(wq);

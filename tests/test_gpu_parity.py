@@ -163,8 +163,11 @@ def test_outlier_stages(name, path):
 def test_full_chain_replay(name, path):
     """12 consecutive sweeps of one chain on the reference's tape (gibbs.py:342-385),
     against the reference's OWN chain: discrete draws exact; the continuous records carry
-    the reference's SVD-mean error (cond(Sigma) ~ 1e8) compounded over
-    the sweeps, hence 1e-6 here.  The 1e-10 check of the same replay is
+    the reference's SVD-mean error compounded over the sweeps, hence
+    max(1e-6, eps x the largest cond(Sigma) of the replay) here -- b normwise per sweep,
+    alpha / pout / theta elementwise.  ECORR models reach cond ~ 2e13, where the reference's
+    own chain is ~1e-4 from the exact algorithm's (0.2 eps cond at most over every fixture,
+    measured with the oracle).  The 1e-10 check of the same replay is
     test_full_chain_replay_vs_oracle."""
     ref = load_ref(name)
     S = int(ref["niter"])
@@ -181,11 +184,13 @@ def test_full_chain_replay(name, path):
     np.testing.assert_array_equal(got["x"], ref["chain"])
     np.testing.assert_array_equal(got["z"], ref["zchain"])
     np.testing.assert_array_equal(got["nu"], ref["dfchain"])
-    tol = 1e-6
-    for k, rk in (("b", "bchain"), ("alpha", "alphachain"), ("pout", "poutchain"),
-                  ("theta", "thetachain")):
+    tol = max(1e-6, np.finfo(float).eps * np.nanmax(ref["tape"]["b_cond"]))
+    nb = np.linalg.norm(ref["bchain"], axis=1)
+    eb = np.linalg.norm(got["b"] - ref["bchain"], axis=1) / np.where(nb > 0, nb, 1.0)
+    assert np.all(eb <= tol), f"b: max normwise rel {eb.max():.3e} > {tol:.1e}"
+    for k, rk in (("alpha", "alphachain"), ("pout", "poutchain"), ("theta", "thetachain")):
         r = _rel(got[k], ref[rk])
-        assert np.all(r <= tol), f"{k}: max rel {r.max():.3e}"
+        assert np.all(r <= tol), f"{k}: max rel {r.max():.3e} > {tol:.1e}"
 
 
 def assert_replay_matches(got, want, ref, label=""):

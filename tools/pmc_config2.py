@@ -19,6 +19,8 @@ def timed(path):
     for r in csv.DictReader(open(path)):
         if "gst_sweep_kernel" in r["Kernel_Name"]:
             by[int(r["Dispatch_Id"])][r["Counter_Name"]] = float(r["Counter_Value"])
+    if not by:          # a pass of another workload (e.g. config 5 in the same directory)
+        return None, {}
     last = max(by)
     return last, by[last]
 
@@ -30,6 +32,8 @@ def main():
     ctr = {}
     for f in sorted(glob.glob(os.path.join(d, "*", "*_counter_collection.csv"))):
         disp, c = timed(f)
+        if disp is None:
+            continue
         ctr.update(c)
         out.setdefault("dispatch", disp)
     rd = 2.0 * ctr["FETCH_SIZE"] * 1024
