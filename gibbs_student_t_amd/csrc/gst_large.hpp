@@ -149,6 +149,9 @@ __device__ __forceinline__ void mh_variate(const DevModel& md, const Rng& rng, c
 }
 
 typedef double XVec[PMAX];   // a chain's parameter vector (x, or an MH proposal)
+// a global-memory double: loads through it are global_load (a generic pointer read out of
+// DevModel compiles to flat_load, which also waits on the LDS counter)
+typedef __attribute__((address_space(1))) double GDouble;
 
 __device__ __forceinline__ double lnpriorP(const DevModel& md, const XVec& xq) {
   bool in = true;
@@ -175,23 +178,32 @@ __device__ __forceinline__ void load_x(const DevModel& md, const DevState& st, i
 // White-noise variances N0_t = efac_b^2 sigma_t^2 + 10^(2 equad_b) of backend b = bk[t]
 // (enterprise MeasurementNoise + EquadNoise, per selection; gibbs.py:154,268,297).  With one
 // backend this is exactly the classic model's expression.
+// The dataset's sigma^2 / backend pointers and nb are copied in (registers): read through
+// md inside a per-TOA loop they were re-loaded every iteration (no machine LICM in this
+// build), each behind a full memory wait.
 struct WhiteNoise {
   double ef2[NBMAX], Q[NBMAX];
-  __device__ __forceinline__ double n0(const DevModel& md, int t) const {
-    if (md.nb <= 1) return ef2[0] * md.sig2[t] + Q[0];
-    const int b = md.bk[t];
+  const double* s2;   // md.sig2
+  const int* bk;      // md.bk (nb > 1)
+  int nb;
+  __device__ __forceinline__ double n0(int t) const {
+    if (nb <= 1) return ef2[0] * s2[t] + Q[0];
+    const int b = bk[t];
     double e = ef2[0], q = Q[0];
 #pragma unroll
     for (int j = 1; j < NBMAX; ++j) {
       e = (b == j) ? ef2[j] : e;
       q = (b == j) ? Q[j] : q;
     }
-    return e * md.sig2[t] + q;
+    return e * s2[t] + q;
   }
 };
 
 __device__ __forceinline__ WhiteNoise white_noise(const DevModel& md, const XVec& x) {
   WhiteNoise w;
+  w.s2 = md.sig2;
+  w.bk = md.bk;
+  w.nb = md.nb;
 #pragma unroll
   for (int b = 0; b < NBMAX; ++b) {
     if (b < md.nb) {
@@ -273,10 +285,38 @@ __global__ void __launch_bounds__(TBLK) lg_white(const DevModel* __restrict__ md
     auto lnl = [&](const WhiteNoise& wn) -> double {
       double sq = 0.0;
       LogProd lp;
-      for (int t = threadIdx.x; t < n; t += TBLK) {
-        const double N0 = wn.n0(md, t);
-        lp.mul(N0);
-        sq += div_pos(wc[t], N0);
+      // one backend: four TOAs' loads in flight per round (the passes were latency-bound at
+      // one load and one full wait per TOA); t order kept, so the sums are unchanged
+      if (wn.nb <= 1) {
+        const double e = wn.ef2[0], q = wn.Q[0];
+        const GDouble* s2 = (const GDouble*)wn.s2;
+        const GDouble* w2 = (const GDouble*)wc;
+        int t = threadIdx.x;
+        for (; t + 3 * TBLK < n; t += 4 * TBLK) {
+          double sv[4], wv[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            sv[k] = s2[t + k * TBLK];
+            wv[k] = w2[t + k * TBLK];
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const double N0 = e * sv[k] + q;
+            lp.mul(N0);
+            sq += div_pos(wv[k], N0);
+          }
+        }
+        for (; t < n; t += TBLK) {
+          const double N0 = e * s2[t] + q;
+          lp.mul(N0);
+          sq += div_pos(w2[t], N0);
+        }
+      } else {
+        for (int t = threadIdx.x; t < n; t += TBLK) {
+          const double N0 = wn.n0(t);
+          lp.mul(N0);
+          sq += div_pos(wc[t], N0);
+        }
       }
       const double sl = block_sum<TBLK / 64>(lp.log_sum(), red);
       sq = block_sum<TBLK / 64>(sq, red);
@@ -316,7 +356,7 @@ __global__ void __launch_bounds__(TBLK) lg_white(const DevModel* __restrict__ md
   for (int t = threadIdx.x; t < npad; t += TBLK) {
     double wt = 0.0;
     if (t < n) {
-      const double N = (zc[t] != 0.0 ? alc[t] : 1.0) * wf.n0(md, t);
+      const double N = (zc[t] != 0.0 ? alc[t] : 1.0) * wf.n0(t);
       lp.mul(N);
       sr += md.resid[t] * md.resid[t] / N;
       wt = 1.0 / N;
@@ -928,7 +968,7 @@ __global__ void __launch_bounds__(TBLK) lg_toa(const DevModel* __restrict__ mds,
   if ((a.mask & 16u) && mix) {
     const double SQ2PI = 2.5066282746310002;  // np.sqrt(2*np.pi)
     for (int t = tid; t < n; t += TBLK) {
-      const double N0 = wn.n0(md, t);
+      const double N0 = wn.n0(t);
       const double Nv = alc[t] * N0;
       const double y = yc[t];
       const double sd1 = sqrt(Nv);
@@ -960,7 +1000,7 @@ __global__ void __launch_bounds__(TBLK) lg_toa(const DevModel* __restrict__ mds,
     if (zs >= 1.0) {
       for (int t = tid; t < n; t += TBLK) {
         const double zf = zc[t] != 0.0 ? 1.0 : 0.0;
-        const double N0 = wn.n0(md, t);
+        const double N0 = wn.n0(t);
         const double top = ((yc[t] * yc[t]) * zf / N0 + nu) / 2.0;
         const double G = tp ? tp[TP_DELTA + m + 1 + nst + t]
                             : gamma_mt((zf + nu) / 2.0, rng, (uint32_t)t, TAG_ALPHA);
