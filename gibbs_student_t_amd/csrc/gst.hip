@@ -586,7 +586,12 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
                eval_only, ow, oh};
   const int nsb = (h.mp / 16 + 3) / 4;
   const int npairs = nsb * (nsb + 1) / 2;
-  const dim3 g_chain(C), b_chain(gst::LBLK), b_toa(gst::TBLK);
+  const bool small_toa = ys <= gst::TBLK_SMALL_NPAD;
+  // hyper blocks of up to HR_COLS (62) columns: one wave per chain, register-resident elimination
+  bool hyper_reg = true;
+  for (const gst::DevModel& hm : cx->hmd) hyper_reg = hyper_reg && hm.nf + hm.nec <= gst::HR_COLS;
+  const dim3 g_hr((C + gst::HR_WPB - 1) / gst::HR_WPB), b_hr(64 * gst::HR_WPB);
+  const dim3 g_chain(C), b_chain(gst::LBLK), b_toa(small_toa ? gst::TBLK_SMALL : gst::TBLK);
   const dim3 g_gram(npairs * ((C + gst::GRAM_WAVES - 1) / gst::GRAM_WAVES)), b_gram(64 * gst::GRAM_WAVES);
   const dim3 g_tb(ys / 64, (C + 63) / 64);
   cx->evused = 0;
@@ -597,7 +602,10 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
   for (int it = 0; it < nit; ++it) {
     a.it = it;
     if (rec_on && it % record_every == 0) LG_LAUNCH(GST_K_RECORD, gst::lg_record, g_chain, b_chain, 0);
-    LG_LAUNCH(GST_K_WHITE, gst::lg_white, g_chain, b_toa, 0);
+    if (small_toa)
+      LG_LAUNCH(GST_K_WHITE, gst::lg_white<gst::TBLK_SMALL>, g_chain, b_toa, 0);
+    else
+      LG_LAUNCH(GST_K_WHITE, gst::lg_white<gst::TBLK>, g_chain, b_toa, 0);
     if ((mask & (6u | GST_STAGE_GRAM)) || eval_only) {
       if (ev_mark(cx, GST_K_GRAM, st, true)) return -1;
       hipLaunchKernelGGL(gst::lg_gram, g_gram, b_gram, gst::GRAM_LDS * 8, st, cx->dmd, a, nsb,
@@ -606,7 +614,10 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
       if (ev_mark(cx, GST_K_GRAM, st, false)) return -1;
       LG_LAUNCH(GST_K_TMELIM, gst::lg_tmelim, g_chain, b_chain, cx->lds_tm);
       if (!(mask & GST_STAGE_GRAM)) {   // timing diagnostic: Gram + TM elimination only
-        LG_LAUNCH(GST_K_HYPER, gst::lg_hyper, g_chain, b_chain, cx->lds_hyper);
+        if (hyper_reg)
+          LG_LAUNCH(GST_K_HYPER, gst::lg_hyper_reg, g_hr, b_hr, 0);
+        else
+          LG_LAUNCH(GST_K_HYPER, gst::lg_hyper, g_chain, b_chain, cx->lds_hyper);
         if (eval_only) break;
         if (mask & 4u) {
           LG_LAUNCH(GST_K_BTM, gst::lg_btm, g_chain, b_chain, cx->lds_btm);
@@ -614,7 +625,12 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
         }
       }
     }
-    if (!eval_only && (mask & 0x78u)) LG_LAUNCH(GST_K_TOA, gst::lg_toa, g_chain, b_toa, 0);
+    if (!eval_only && (mask & 0x78u)) {
+      if (small_toa)
+        LG_LAUNCH(GST_K_TOA, gst::lg_toa<gst::TBLK_SMALL>, g_chain, b_toa, 0);
+      else
+        LG_LAUNCH(GST_K_TOA, gst::lg_toa<gst::TBLK>, g_chain, b_toa, 0);
+    }
   }
   HIP_OK(hipEventRecord(cx->ev1, st));
   cx->timed = true;

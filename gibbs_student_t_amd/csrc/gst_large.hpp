@@ -31,7 +31,14 @@
 namespace gst {
 
 constexpr int LBLK = 256;      // threads of the per-chain kernels (4 waves)
-constexpr int TBLK = 1024;     // per-chain per-TOA passes (white, toa): 16 waves hide latency
+// threads per chain of the per-TOA passes (lg_white, lg_toa): 16 waves per chain for the
+// 100k-TOA datasets; 4 for datasets of up to TBLK_SMALL_NPAD TOAs, where a pass is a few
+// TOAs per thread and a 16-wave chain spent it in barriers and reductions with one chain per
+// CU.  Chosen from the datasets alone (never from the chain count), so the chains do not
+// depend on how a launch is sharded.
+constexpr int TBLK = 1024;
+constexpr int TBLK_SMALL = 256;
+constexpr int TBLK_SMALL_NPAD = 32768;
 constexpr int GRAM_WAVES = 8;  // chains per gram workgroup
 constexpr int TM_PW = 16;      // panel width of the timing-model elimination
 
@@ -246,13 +253,14 @@ __global__ void __launch_bounds__(LBLK) lg_record(const DevModel* __restrict__ m
 // ------------------------------------------------------------------------------------
 // white: MH over the white-noise parameters, then N^-1 for the Gram
 // ------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(TBLK) lg_white(const DevModel* __restrict__ mds, LArgs a) {
+template <int TB>
+__global__ void __launch_bounds__(TB) lg_white(const DevModel* __restrict__ mds, LArgs a) {
   const int c = blockIdx.x;
   const DevModel& md = mds[ds_of(a, c)];
   if (threadIdx.x == 0 && a.st.dataset && a.st.status &&
       (unsigned)a.st.dataset[c] >= (unsigned)a.st.nd)
     a.st.status[c] |= 4;                          // bad dataset index (ran on dataset 0)
-  __shared__ double red[TBLK / 64];
+  __shared__ double red[TB / 64];
   __shared__ double mhv[NWHITE][4];
   const int n = md.n, nst = a.st.nst, npad = md.npad;
   const double* zc = a.st.z + (size_t)c * nst;
@@ -270,13 +278,13 @@ __global__ void __launch_bounds__(TBLK) lg_white(const DevModel* __restrict__ md
   if (do_white) {
     // fixed over the block: a_t = alpha_t^z_t, y_t^2 / a_t and sum log a_t
     double la = 0.0;
-    for (int t = threadIdx.x; t < n; t += TBLK) {
+    for (int t = threadIdx.x; t < n; t += TB) {
       const bool zt = zc[t] != 0.0;
       const double at = zt ? alc[t] : 1.0;
       if (zt) la += log(at);
       wc[t] = yc[t] * yc[t] / at;
     }
-    la = block_sum<TBLK / 64>(la, red);
+    la = block_sum<TB / 64>(la, red);
     if (!a.eval_only && threadIdx.x < NWHITE) mh_variate(md, rng, tp, threadIdx.x, mhv[threadIdx.x]);
     __syncthreads();
     // a proposal's variances come from its parameters, except that Q of a one-backend model
@@ -292,12 +300,12 @@ __global__ void __launch_bounds__(TBLK) lg_white(const DevModel* __restrict__ md
         const GDouble* s2 = (const GDouble*)wn.s2;
         const GDouble* w2 = (const GDouble*)wc;
         int t = threadIdx.x;
-        for (; t + 3 * TBLK < n; t += 4 * TBLK) {
+        for (; t + 3 * TB < n; t += 4 * TB) {
           double sv[4], wv[4];
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            sv[k] = s2[t + k * TBLK];
-            wv[k] = w2[t + k * TBLK];
+            sv[k] = s2[t + k * TB];
+            wv[k] = w2[t + k * TB];
           }
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
@@ -306,20 +314,20 @@ __global__ void __launch_bounds__(TBLK) lg_white(const DevModel* __restrict__ md
             sq += div_pos(wv[k], N0);
           }
         }
-        for (; t < n; t += TBLK) {
+        for (; t < n; t += TB) {
           const double N0 = e * s2[t] + q;
           lp.mul(N0);
           sq += div_pos(w2[t], N0);
         }
       } else {
-        for (int t = threadIdx.x; t < n; t += TBLK) {
+        for (int t = threadIdx.x; t < n; t += TB) {
           const double N0 = wn.n0(t);
           lp.mul(N0);
           sq += div_pos(wc[t], N0);
         }
       }
-      const double sl = block_sum<TBLK / 64>(lp.log_sum(), red);
-      sq = block_sum<TBLK / 64>(sq, red);
+      const double sl = block_sum<TB / 64>(lp.log_sum(), red);
+      sq = block_sum<TB / 64>(sq, red);
       return -0.5 * ((la + sl) + sq);
     };
     WhiteNoise wx = white_noise(md, xv);
@@ -353,7 +361,7 @@ __global__ void __launch_bounds__(TBLK) lg_white(const DevModel* __restrict__ md
   const WhiteNoise wf = white_noise(md, xv);
   double sr = 0.0;
   LogProd lp;
-  for (int t = threadIdx.x; t < npad; t += TBLK) {
+  for (int t = threadIdx.x; t < npad; t += TB) {
     double wt = 0.0;
     if (t < n) {
       const double N = (zc[t] != 0.0 ? alc[t] : 1.0) * wf.n0(t);
@@ -363,8 +371,8 @@ __global__ void __launch_bounds__(TBLK) lg_white(const DevModel* __restrict__ md
     }
     wc[t] = wt;
   }
-  const double sl = block_sum<TBLK / 64>(lp.log_sum(), red);
-  sr = block_sum<TBLK / 64>(sr, red);
+  const double sl = block_sum<TB / 64>(lp.log_sum(), red);
+  sr = block_sum<TB / 64>(sr, red);
   if (threadIdx.x == 0) {
     sc[SC_LOGDETN] = sl;
     sc[SC_RNR] = sr;
@@ -827,6 +835,219 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
 }
 
 // ------------------------------------------------------------------------------------
+// hyper, register-resident (hyper block of at most HR_COLS = 62 columns): one wave per chain runs
+// lg_hyper's MH with the persistent kernel's elimination (gst_kernel.hpp chol_range: 8x8-
+// cyclic register layout, one published column per LDS hand-off) instead of an LDS
+// factorisation with a workgroup barrier per column.  Internal order: the nf hyper columns,
+// unit-prior dummies up to HR_RA (exact no-ops: zero coupling, pivot 1), the augmented row
+// at HR_RA, one zero pad row.  Same variates, MH decisions and outputs (x, status, v's Fourier block, the
+// redraw flags) as lg_hyper; the likelihood sums run in the persistent kernel's order.
+// ------------------------------------------------------------------------------------
+constexpr int HR_MT = 8;                          // 64 internal rows
+constexpr int HR_RA = 8 * HR_MT - 2;              // augmented row (the paired tail covers an
+                                                  // even number of columns from slot KP)
+constexpr int HR_COLS = HR_RA;                    // hyper columns it takes (nf + nec)
+constexpr int HR_WPB = 4;                         // chains (waves) per workgroup
+constexpr int HR_S0 = 64 * SL(HR_MT, 0);          // S0 [slot][lane]
+constexpr int HR_LDS = HR_S0 + 8 * HR_MT /*colq*/ + 8 * HR_MT /*junk*/ +
+                       8 * pair_pw(HR_MT) /*colq2*/ + 64 /*phi^-1*/ + 4 * NHYPER /*mhv*/ +
+                       64 /*rhs*/;
+
+__global__ void __launch_bounds__(64 * HR_WPB) lg_hyper_reg(const DevModel* __restrict__ mds,
+                                                              LArgs a) {
+  constexpr int MT = HR_MT, RA = HR_RA, NSL = SL(MT, 0);
+  __shared__ double smem[HR_WPB][HR_LDS];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = blockIdx.x * HR_WPB + wv;
+  if (c >= a.C) return;
+  const DevModel& md = mds[ds_of(a, c)];
+  double* S0R = smem[wv];
+  double* colq = S0R + HR_S0;
+  double* junk = colq + 8 * MT;
+  double* colq2 = junk + 8 * MT;
+  double* ph = colq2 + 8 * pair_pw(MT);
+  double* mhv = ph + 64;
+  double* rhs = mhv + 4 * NHYPER;
+  const int p = lane >> 3, q = lane & 7;
+  const int nf = md.nf + md.nec, nfr = md.nf, K0 = md.ntm_pad, mp = md.mp;
+  double* sc = a.s.sc + (size_t)c * 16;
+  const double* Gc = a.s.G + (size_t)c * mp * mp;
+  const Rng rng = make_rng(a, c);
+  const double* tp = tape_row(a, c);
+  XVec xv;
+  load_x(md, a.st, c, xv);
+  const double logdetN = sc[SC_LOGDETN], rNr = sc[SC_RNR];
+  const double ld_tm = sc[SC_LDTM], quad_tm = sc[SC_QUADTM];
+  const int fail_tm = sc[SC_FAILTM] != 0.0;
+  const double x_last0 = sc[SC_XLAST];
+  int status = fail_tm ? 1 : 0;
+  if (!a.eval_only && lane < NHYPER) mh_variate(md, rng, tp, NWHITE + lane, mhv + 4 * lane);
+  // S0 from the Gram's trailing block (lg_tmelim left the Schur complement there), in the
+  // cyclic layout: slot (r, s), lane (p, q) = internal (8r+p, 8s+q); diagonal slots hold the
+  // full symmetric 8x8 block
+  auto gidx = [&](int i) __attribute__((always_inline)) { return i < nf ? K0 + i : (i == RA ? md.raug : -1); };
+#pragma unroll
+  for (int r = 0; r < MT; ++r)
+#pragma unroll
+    for (int s2 = 0; s2 <= r; ++s2) {
+      int i = 8 * r + p, j = 8 * s2 + q;
+      if (j > i) { const int t = i; i = j; j = t; }
+      const int gi = gidx(i), gj = gidx(j);
+      double v = (i == j) ? 1.0 : 0.0;
+      if (gi >= 0 && gj >= 0) v = Gc[(size_t)gi * mp + gj];
+      S0R[64 * SL(r, s2) + lane] = v;
+    }
+  double L[NSL];
+  double apr[2] = {1.0, 1.0}, zr[2] = {0.0, 0.0};
+  // factor S0 + diag(phi^-1(q)) in registers; the b-marginalised lnL (gibbs.py:288-329)
+  auto lnl = [&](const XVec& xq, int& failed) __attribute__((always_inline)) -> double {
+    const double lA = xget(xq, md.idx_logA);
+    const double g = xget(xq, md.idx_gamma);
+    const double lc = 2.0 * lA * 2.302585092994045684 - md.log_12pi2 + (g - 3.0) * md.log_fyr;
+    double pv = 0.0;                    // phi^-1 of internal column `lane` (0: none)
+    if (lane < nfr) {
+      pv = exp(-(lc - g * md.lfreq[lane] + md.ldf[lane]));
+    } else if (lane < nf) {
+      const int b = md.ecb[lane - nfr];
+      int pi = md.ecorr_b[0];
+#pragma unroll
+      for (int j = 1; j < NBMAX; ++j) pi = (b == j) ? md.ecorr_b[j] : pi;
+      pv = exp(-2.0 * xget(xq, pi) * 2.302585092994045684);
+    }
+    ph[lane] = pv;
+    double logdet_phi = ((double)nfr * lc - g * md.sum_lfreq + md.sum_ldf) + md.logdet_phi_tm;
+    for (int b = 0; b < md.nb; ++b)
+      if (md.ec_count[b] > 0.0)
+        logdet_phi += md.ec_count[b] * (2.0 * xget(xq, md.ecorr_b[b]) * 2.302585092994045684);
+    lds_order();
+#pragma unroll
+    for (int r = 0; r < MT; ++r)
+#pragma unroll
+      for (int s2 = 0; s2 <= r; ++s2) {
+        double v = S0R[64 * SL(r, s2) + lane];
+        if (r == s2 && p == q) v += ph[8 * r + p];
+        L[SL(r, s2)] = v;
+      }
+    CholCtx cc{colq, junk, colq2, lane, p, q, RA, 1.0, 0.0, 0, 0, {1.0, 1.0}, {0.0, 0.0}};
+    chol_range<MT, 0, RA, kp_for(1)>(L, cc);
+    chol_harvest<MT, 0, RA, RA>(L, cc);
+    chol_stats<0, RA>(cc);
+    apr[0] = cc.apr[0];
+    zr[0] = cc.zr[0];
+    failed = cc.fail | fail_tm;
+    if (failed) return -INFINITY;
+    const double ld = log(cc.mant) + (double)cc.expo * 0.693147180559945309417;
+    double ll = -0.5 * (logdetN + rNr);
+    ll += 0.5 * ((quad_tm + cc.quad) - (ld_tm + ld) - logdet_phi);
+    return ll;
+  };
+
+  const bool run = (a.mask & 6u) || a.eval_only;
+  bool redraw = false, Lvalid = false;
+  int fb = 0;
+  lds_order();
+  if (run) {
+    double l0 = 0.0, p0 = 0.0;
+    const int first = ((a.mask & 2u) || a.eval_only) ? -1 : NHYPER;
+    for (int step = first; step <= NHYPER; ++step) {
+      XVec xq;
+      double luacc = 0.0;
+      if (step == NHYPER) {
+        if (a.eval_only || !(a.mask & 4u)) break;
+        redraw = true;
+#pragma unroll
+        for (int j = 0; j < PMAX; ++j)
+          if (j < md.P) redraw = redraw && (xv[j] != x_last0);   // gibbs.py:373
+        if (a.mask & 128u) redraw = true;
+        if (!redraw || Lvalid) break;
+      }
+      if (step < 0 || step == NHYPER) {
+#pragma unroll
+        for (int j = 0; j < PMAX; ++j) xq[j] = xv[j];
+      } else {
+        const int par = (int)mhv[4 * step + 0];
+        const double delta = mhv[4 * step + 1];
+#pragma unroll
+        for (int j = 0; j < PMAX; ++j) xq[j] = (j == par) ? xv[j] + delta : xv[j];
+        luacc = mhv[4 * step + 2];
+      }
+      const double p1 = lnpriorP(md, xq);
+      if (step >= 0 && step < NHYPER && p1 == -INFINITY) continue;
+      int f1 = 0;
+      const double l1 = lnl(xq, f1);
+      if (step == NHYPER) {
+        fb = f1;
+        break;
+      }
+      if (f1) status |= 1;
+      if (step < 0) {
+        l0 = l1;
+        p0 = p1;
+        Lvalid = !f1;   // see lg_hyper
+        if (a.eval_only) {
+          if (lane == 0) a.out_h[c] = l1;
+          break;
+        }
+        continue;
+      }
+      if ((l1 + p1) - (l0 + p0) > luacc) {
+#pragma unroll
+        for (int j = 0; j < PMAX; ++j) xv[j] = xq[j];
+        l0 = l1;
+        p0 = p1;
+        Lvalid = true;
+      } else {
+        Lvalid = false;
+      }
+    }
+  }
+  if (a.eval_only) return;
+  if (lane < md.P) a.st.x[(size_t)c * md.P + lane] = xget(xv, lane);
+  if (lane == 0) {
+    sc[SC_REDRAW] = redraw ? 1.0 : 0.0;
+    sc[SC_FB] = (double)fb;
+    if (a.st.status) a.st.status[c] |= status | ((redraw && fb) ? 2 : 0);
+  }
+  if (!redraw || fb) return;
+  // b draw, hyper block (lg_hyper's back substitution): the raw factor goes to the S0 region
+  // ([slot][lane]: a_ik at 64 SL(i/8, k/8) + 8 (i%8) + k%8); lane k owns column k
+#pragma unroll
+  for (int sl = 0; sl < NSL; ++sl) S0R[64 * sl + lane] = L[sl];
+  lds_order();
+  auto aik = [&](int i, int k) __attribute__((always_inline)) { return S0R[64 * SL(i >> 3, k >> 3) + 8 * (i & 7) + (k & 7)]; };
+  const int k = lane;
+  const bool kin = k < nf;
+  const double akk = apr[0];            // pivot of column `lane` (chol_harvest)
+  const double yk = kin ? rsqrt_nr(akk) : 0.0;
+  double w = 0.0;
+  if (tp) {
+    rhs[k] = 0.0;
+    lds_order();
+    for (int j = lane; j < md.m; j += 64) {
+      const int ii = md.ref2int[j] - K0;
+      if (ii >= 0 && ii < nf) rhs[ii] = tp[TP_DELTA + j];
+    }
+    lds_order();
+    // eta_k = y_k sum_{i >= k} a_ik Delta_i (so that L^-T eta = Delta)
+    double sacc = 0.0;
+    if (kin)
+      for (int i = k; i < nf; ++i) sacc += aik(i, k) * rhs[i];
+    w = (zr[0] + sacc) * yk;
+  } else if (kin) {
+    w = zr[0] * yk + normal_k(rng, (uint32_t)(K0 + k), TAG_BDRAW);
+  }
+  double* vF = a.s.v + (size_t)c * mp + K0;
+  double acc = 0.0;                     // acc_k = sum_{i > k} a_ik v_i
+  for (int i = nf - 1; i >= 0; --i) {
+    const double yi = rdlane(yk, i), wi = rdlane(w, i), ai = rdlane(acc, i);
+    const double vi = (wi - yi * ai) * yi;
+    if (lane == 0) vF[i] = vi;
+    if (k < i) acc += aik(i, k) * vi;
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // btm: b draw's timing-model block, L^T v = w over columns [0, K0) with rows up to raug
 // ------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(LBLK) lg_btm(const DevModel* __restrict__ mds, LArgs a) {
@@ -934,10 +1155,11 @@ __global__ void __launch_bounds__(LBLK) lg_tb(const DevModel* __restrict__ mds, 
 // ------------------------------------------------------------------------------------
 // toa: theta, z, alpha, nu (gibbs.py:185-259)
 // ------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(TBLK) lg_toa(const DevModel* __restrict__ mds, LArgs a) {
+template <int TB>
+__global__ void __launch_bounds__(TB) lg_toa(const DevModel* __restrict__ mds, LArgs a) {
   const int c = blockIdx.x;
   const DevModel& md = mds[ds_of(a, c)];
-  __shared__ double red[TBLK / 64];
+  __shared__ double red[TB / 64];
   __shared__ double dfb[32];
   const int n = md.n, nst = a.st.nst, m = md.m, tid = threadIdx.x;
   double* zc = a.st.z + (size_t)c * nst;
@@ -953,8 +1175,8 @@ __global__ void __launch_bounds__(TBLK) lg_toa(const DevModel* __restrict__ mds,
   const bool mix = (md.model == 2) || (md.model == 3);
   if ((a.mask & 8u) && mix) {
     double zs = 0.0;
-    for (int t = tid; t < n; t += TBLK) zs += (zc[t] != 0.0) ? 1.0 : 0.0;
-    zs = block_sum<TBLK / 64>(zs, red);
+    for (int t = tid; t < n; t += TB) zs += (zc[t] != 0.0) ? 1.0 : 0.0;
+    zs = block_sum<TB / 64>(zs, red);
     const double aa = zs + md.mk;
     const double bb = ((double)n - zs) + md.k1mm;
     if (tp) {
@@ -967,7 +1189,7 @@ __global__ void __launch_bounds__(TBLK) lg_toa(const DevModel* __restrict__ mds,
   }
   if ((a.mask & 16u) && mix) {
     const double SQ2PI = 2.5066282746310002;  // np.sqrt(2*np.pi)
-    for (int t = tid; t < n; t += TBLK) {
+    for (int t = tid; t < n; t += TB) {
       const double N0 = wn.n0(t);
       const double Nv = alc[t] * N0;
       const double y = yc[t];
@@ -995,10 +1217,10 @@ __global__ void __launch_bounds__(TBLK) lg_toa(const DevModel* __restrict__ mds,
   __syncthreads();
   if ((a.mask & 32u) && md.vary_alpha) {
     double zs = 0.0;
-    for (int t = tid; t < n; t += TBLK) zs += (zc[t] != 0.0) ? 1.0 : 0.0;
-    zs = block_sum<TBLK / 64>(zs, red);
+    for (int t = tid; t < n; t += TB) zs += (zc[t] != 0.0) ? 1.0 : 0.0;
+    zs = block_sum<TB / 64>(zs, red);
     if (zs >= 1.0) {
-      for (int t = tid; t < n; t += TBLK) {
+      for (int t = tid; t < n; t += TB) {
         const double zf = zc[t] != 0.0 ? 1.0 : 0.0;
         const double N0 = wn.n0(t);
         const double top = ((yc[t] * yc[t]) * zf / N0 + nu) / 2.0;
@@ -1012,11 +1234,11 @@ __global__ void __launch_bounds__(TBLK) lg_toa(const DevModel* __restrict__ mds,
   if ((a.mask & 64u) && md.vary_df) {
     double sa = 0.0;
     LogProd lp;
-    for (int t = tid; t < n; t += TBLK) {
+    for (int t = tid; t < n; t += TB) {
       lp.mul(alc[t]);
       sa += 1.0 / alc[t];
     }
-    const double S = block_sum<TBLK / 64>(lp.log_sum() + sa, red);
+    const double S = block_sum<TB / 64>(lp.log_sum() + sa, red);
     if (tid < 64) {
       double ll = -INFINITY;
       if (tid < 30) {
