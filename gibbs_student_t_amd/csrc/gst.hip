@@ -591,6 +591,12 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
   bool hyper_reg = true;
   for (const gst::DevModel& hm : cx->hmd) hyper_reg = hyper_reg && hm.nf + hm.nec <= gst::HR_COLS;
   const dim3 g_hr((C + gst::HR_WPB - 1) / gst::HR_WPB), b_hr(64 * gst::HR_WPB);
+  // Grams of at most GS_NTMAX 16-column tiles: one wave per chain (lg_gram_small<NT>)
+  int gram_small = h.mp / 16;
+  for (const gst::DevModel& hm : cx->hmd)
+    if (hm.mp != h.mp) gram_small = 0;
+  if (gram_small > gst::GS_NTMAX) gram_small = 0;
+  const dim3 g_gs((C + gst::GS_WPB - 1) / gst::GS_WPB), b_gs(64 * gst::GS_WPB);
   const dim3 g_chain(C), b_chain(gst::LBLK), b_toa(small_toa ? gst::TBLK_SMALL : gst::TBLK);
   const dim3 g_gram(npairs * ((C + gst::GRAM_WAVES - 1) / gst::GRAM_WAVES)), b_gram(64 * gst::GRAM_WAVES);
   const dim3 g_tb(ys / 64, (C + 63) / 64);
@@ -608,8 +614,17 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
       LG_LAUNCH(GST_K_WHITE, gst::lg_white<gst::TBLK>, g_chain, b_toa, 0);
     if ((mask & (6u | GST_STAGE_GRAM)) || eval_only) {
       if (ev_mark(cx, GST_K_GRAM, st, true)) return -1;
-      hipLaunchKernelGGL(gst::lg_gram, g_gram, b_gram, gst::GRAM_LDS * 8, st, cx->dmd, a, nsb,
-                         npairs);
+      switch (gram_small) {
+        case 1: hipLaunchKernelGGL(gst::lg_gram_small<1>, g_gs, b_gs, 0, st, cx->dmd, a); break;
+        case 2: hipLaunchKernelGGL(gst::lg_gram_small<2>, g_gs, b_gs, 0, st, cx->dmd, a); break;
+        case 3: hipLaunchKernelGGL(gst::lg_gram_small<3>, g_gs, b_gs, 0, st, cx->dmd, a); break;
+        case 4: hipLaunchKernelGGL(gst::lg_gram_small<4>, g_gs, b_gs, 0, st, cx->dmd, a); break;
+        case 5: hipLaunchKernelGGL(gst::lg_gram_small<5>, g_gs, b_gs, 0, st, cx->dmd, a); break;
+        case 6: hipLaunchKernelGGL(gst::lg_gram_small<6>, g_gs, b_gs, 0, st, cx->dmd, a); break;
+        default:
+          hipLaunchKernelGGL(gst::lg_gram, g_gram, b_gram, gst::GRAM_LDS * 8, st, cx->dmd, a, nsb,
+                             npairs);
+      }
       HIP_OK(hipGetLastError());
       if (ev_mark(cx, GST_K_GRAM, st, false)) return -1;
       LG_LAUNCH(GST_K_TMELIM, gst::lg_tmelim, g_chain, b_chain, cx->lds_tm);

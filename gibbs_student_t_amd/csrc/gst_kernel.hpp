@@ -33,6 +33,9 @@
 namespace gst {
 
 typedef double v4d __attribute__((ext_vector_type(4)));
+// a global-memory double: loads through it are global_load (a generic pointer read out of
+// DevModel compiles to flat_load, which also waits on the LDS counter)
+typedef __attribute__((address_space(1))) double GDouble;
 
 constexpr int NWHITE = 20;
 constexpr int NHYPER = 10;
@@ -1220,7 +1223,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       // its MFMAs have issued, so a T load has two k-steps (30 MFMAs) to arrive from L2
       double ta[NT], tb[NT], wa, wb;
       auto tload = [&](double (&t)[NT], double& w, int ks) __attribute__((always_inline)) {
-        const double* src = md.Tmf + (size_t)ks * NT * 64;
+        const GDouble* src = (const GDouble*)md.Tmf + (size_t)ks * NT * 64;
 #pragma unroll
         for (int X = 0; X < NT; ++X) t[X] = src[X * 64 + lane];
         w = vbuf[4 * ks + tl];
@@ -1236,17 +1239,25 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
           }
         }
       };
+      // an even number of k-steps (Tmf and the weights are zero past n: a padding k-step
+      // adds exact zeros), so the loop body has no conditional load and the wait before a
+      // set's MFMAs covers only that set (a branch in the body made the compiler wait for
+      // both sets at the top of every iteration); the scheduling barriers keep the order
+      const int nksp = (md.nks + 1) & ~1;
       tload(ta, wa, 0);
-      if (md.nks > 1) tload(tb, wb, 1);
+      tload(tb, wb, 1);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll 1
-      for (int ks = 0; ks < md.nks; ks += 2) {
+      for (int ks = 0; ks + 2 < nksp; ks += 2) {
         kstep(ta, wa);
-        if (ks + 2 < md.nks) tload(ta, wa, ks + 2);
-        if (ks + 1 < md.nks) {
-          kstep(tb, wb);
-          if (ks + 3 < md.nks) tload(tb, wb, ks + 3);
-        }
+        tload(ta, wa, ks + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        kstep(tb, wb);
+        tload(tb, wb, ks + 3);
+        __builtin_amdgcn_sched_barrier(0);
       }
+      kstep(ta, wa);
+      kstep(tb, wb);
       GST_SUB_END(9)
       // MFMA C layout (col = lane&15, row = lane>>4 + 4 reg) -> cyclic register layout
       if constexpr (OWN == 0) {
@@ -1317,7 +1328,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     // its MFMAs have issued, so a T load has two k-steps (30 MFMAs) to arrive from L2
     double ta[NT], tb[NT], wa, wb;
     auto tload = [&](double (&t)[NT], double& w, int ks) __attribute__((always_inline)) {
-      const double* src = md.Tmf + (size_t)ks * NT * 64;
+      const GDouble* src = (const GDouble*)md.Tmf + (size_t)ks * NT * 64;
 #pragma unroll
       for (int X = 0; X < NT; ++X) t[X] = src[X * 64 + lane];
       w = vbuf[4 * ks + tl];
@@ -1333,17 +1344,25 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         }
       }
     };
+    // an even number of k-steps (Tmf and the weights are zero past n: a padding k-step
+    // adds exact zeros), so the loop body has no conditional load and the wait before a
+    // set's MFMAs covers only that set (a branch in the body made the compiler wait for
+    // both sets at the top of every iteration); the scheduling barriers keep the order
+    const int nksp = (md.nks + 1) & ~1;
     tload(ta, wa, 0);
-    if (md.nks > 1) tload(tb, wb, 1);
+    tload(tb, wb, 1);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll 1
-    for (int ks = 0; ks < md.nks; ks += 2) {
+    for (int ks = 0; ks + 2 < nksp; ks += 2) {
       kstep(ta, wa);
-      if (ks + 2 < md.nks) tload(ta, wa, ks + 2);
-      if (ks + 1 < md.nks) {
-        kstep(tb, wb);
-        if (ks + 3 < md.nks) tload(tb, wb, ks + 3);
-      }
+      tload(ta, wa, ks + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      kstep(tb, wb);
+      tload(tb, wb, ks + 3);
+      __builtin_amdgcn_sched_barrier(0);
     }
+    kstep(ta, wa);
+    kstep(tb, wb);
     GST_SUB_END(9)
     // MFMA C layout (col = lane&15, row = lane>>4 + 4 reg) -> cyclic register layout
 #pragma unroll

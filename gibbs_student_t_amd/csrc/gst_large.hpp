@@ -156,9 +156,6 @@ __device__ __forceinline__ void mh_variate(const DevModel& md, const Rng& rng, c
 }
 
 typedef double XVec[PMAX];   // a chain's parameter vector (x, or an MH proposal)
-// a global-memory double: loads through it are global_load (a generic pointer read out of
-// DevModel compiles to flat_load, which also waits on the LDS counter)
-typedef __attribute__((address_space(1))) double GDouble;
 
 __device__ __forceinline__ double lnpriorP(const DevModel& md, const XVec& xq) {
   bool in = true;
@@ -547,6 +544,82 @@ __global__ void __launch_bounds__(64 * GRAM_WAVES) lg_gram(const DevModel* __res
       default: gram_tile<1, true>(md, a, Tl, Wl, I, J, c, live); break;
     }
   }
+}
+
+// ------------------------------------------------------------------------------------
+// gram, small models (mp <= 16 GS_NTMAX): one wave per chain computes every lower tile of its
+// Gram, T streamed from L2 with two k-steps of operands in flight (the persistent kernel's
+// Gram loop, weights from the white pass's w row).  With a few 16-column tiles the 64x64
+// super-tiles of lg_gram split the lower triangle unevenly between their workgroups (m ~ 75:
+// 10 / 4 / 1 tiles), and the diagonal one set the time.  Every tile receives the same MFMA
+// sequence as in lg_gram (k-steps in order, A = T w, B = T), so G is bitwise lg_gram's.
+// ------------------------------------------------------------------------------------
+constexpr int GS_NTMAX = 6;
+constexpr int GS_WPB = 4;
+constexpr int GS_DEPTH = 4;
+template <int NT>
+__global__ void __launch_bounds__(64 * GS_WPB) lg_gram_small(const DevModel* __restrict__ mds,
+                                                               LArgs a) {
+  constexpr int NTT = NT * (NT + 1) / 2;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * GS_WPB + (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (c >= a.C) return;
+  const DevModel& md = mds[ds_of(a, c)];
+  const int tl = lane >> 4, nks = md.npad / 4, mp = md.mp;
+  const GDouble* wc = (const GDouble*)(a.s.w + (size_t)c * a.ys);
+  const GDouble* Tm = (const GDouble*)md.Tmf;
+  v4d acc[NTT];
+#pragma unroll
+  for (int i = 0; i < NTT; ++i) acc[i] = (v4d){0.0, 0.0, 0.0, 0.0};
+  // GS_DEPTH k-steps of operands in flight: a set is reloaded right after its MFMAs issue, so
+  // its loads have GS_DEPTH - 1 k-steps of MFMAs (T misses L2 beyond ~4k TOAs) to arrive
+  constexpr int D = GS_DEPTH;
+  double t[D][NT], w[D];
+  auto tload = [&](double (&tt)[NT], double& ww, int ks) __attribute__((always_inline)) {
+#pragma unroll
+    for (int X = 0; X < NT; ++X) tt[X] = Tm[((size_t)ks * NT + X) * 64 + lane];
+    ww = wc[4 * ks + tl];
+  };
+  auto kstep = [&](const double (&t)[NT], const double wt) __attribute__((always_inline)) {
+#pragma unroll
+    for (int I = 0; I < NT; ++I) {
+      const double av = t[I] * wt;
+#pragma unroll
+      for (int J = 0; J <= I; ++J)
+        acc[I * (I + 1) / 2 + J] =
+            __builtin_amdgcn_mfma_f64_16x16x4f64(av, t[J], acc[I * (I + 1) / 2 + J], 0, 0, 0);
+    }
+  };
+  // nks = npad / 4 is a multiple of 16: the main loop has no conditional load, so the
+  // compiler's wait counts keep the later sets' loads in flight (a branch in the body made
+  // it wait for every load at the top of each iteration)
+  static_assert(16 % D == 0, "k-step count is a multiple of 16");
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    tload(t[d], w[d], d);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  int ks = 0;
+  for (; ks + D < nks; ks += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      kstep(t[d], w[d]);
+      tload(t[d], w[d], ks + d + D);
+      // keep the k-steps in program order: the scheduler otherwise hoists all four sets'
+      // weight multiplies to the top of the body, i.e. waits for every load there
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d) kstep(t[d], w[d]);
+  double* Gc = a.s.G + (size_t)c * mp * mp;
+#pragma unroll
+  for (int I = 0; I < NT; ++I)
+#pragma unroll
+    for (int J = 0; J <= I; ++J)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        Gc[(size_t)(16 * I + tl + 4 * g) * mp + 16 * J + (lane & 15)] = acc[I * (I + 1) / 2 + J][g];
 }
 
 // ------------------------------------------------------------------------------------

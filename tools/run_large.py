@@ -1,6 +1,6 @@
 """Short config-5 run of the large path for profiling (rocprofv3 -- python tools/run_large.py).
 
-    python tools/run_large.py [sweeps] [chains] [n] [components] [ntm]
+    python tools/run_large.py [sweeps] [chains] [n] [components] [ntm] [warmup sweeps]
 """
 import sys
 import time
@@ -25,9 +25,13 @@ def main():
     ns = NativeSampler(pta, CFG, 0)
     ns.alloc(C)
     ns.set_state(**initial_state(pta, C, 0))
+    W = int(sys.argv[6]) if len(sys.argv) > 6 else 0
+    if W:   # untimed warmup sweeps (the clock ramps out of idle over the first milliseconds)
+        ns.sweep(W, seed=1)
+        ns.synchronize()
     ns.set_timing(True)
     t0 = time.perf_counter()
-    ns.sweep(S, seed=1)
+    ns.sweep(S, seed=1, sweep0=W)
     ns.synchronize()
     dt = time.perf_counter() - t0
     kt = ns.kernel_times()
