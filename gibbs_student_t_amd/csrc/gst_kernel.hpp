@@ -1429,6 +1429,11 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     const double g = pget(xq, md.idx_gamma);
     // log phi_k = 2 lA ln10 - log(12 pi^2) + (g-3) log fyr - g log f_k + log df_k
     const double lc = 2.0 * lA * 2.302585092994045684 - md.log_12pi2 + (g - 3.0) * md.log_fyr;
+    // S0 first: its 36 LDS loads are in flight while phi^-1 is computed (exp)
+#pragma unroll
+    for (int r = K0; r < MT; ++r)
+#pragma unroll
+      for (int s = K0; s <= r; ++s) L[SL(r, s)] = S0[64 * SL(r - K0, s - K0)];
     // Fourier columns, then the unit-prior dummies that pad a smaller model up to this
     // instance's RA (zero Gram rows: each is eliminated as an exact no-op)
     if (lane < RA - md.ntm_pad)
@@ -1442,12 +1447,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     lds_order();
 #pragma unroll
     for (int r = K0; r < MT; ++r)
-#pragma unroll
-      for (int s = K0; s <= r; ++s) {
-        double v = S0[64 * SL(r - K0, s - K0)];
-        if (r == s && p == q) v += phbuf[8 * r + p];
-        L[SL(r, s)] = v;
-      }
+      if (p == q) L[SL(r, r)] += phbuf[8 * r + p];
     CholCtx cc{colq, phbuf, colq2, lane, p, q, raug, 1.0, 0.0, 0, 0, {tm_apr, 1.0}, {tm_zr, 0.0}};
     GST_SUB_END(7)
     chol_range<MT, K0, RA, kp_for(OCC)>(L, cc);

@@ -16,7 +16,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEYS = ("x", "b", "z", "alpha", "pout", "theta", "nu")
-CASES = ("j1713", "c3", "c20", "tm22")
+CASES = tuple(os.environ.get("AB_CASES", "j1713,c3,c20,tm22").split(","))
 
 
 def worker(case, C, S, out):
