@@ -608,7 +608,9 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
   for (int it = 0; it < nit; ++it) {
     a.it = it;
     if (rec_on && it % record_every == 0) LG_LAUNCH(GST_K_RECORD, gst::lg_record, g_chain, b_chain, 0);
-    if (small_toa)
+    if (ys <= gst::TBLK_WAVE_NPAD)
+      LG_LAUNCH(GST_K_WHITE, gst::lg_white<gst::TBLK_WAVE>, g_chain, dim3(gst::TBLK_WAVE), 0);
+    else if (small_toa)
       LG_LAUNCH(GST_K_WHITE, gst::lg_white<gst::TBLK_SMALL>, g_chain, b_toa, 0);
     else
       LG_LAUNCH(GST_K_WHITE, gst::lg_white<gst::TBLK>, g_chain, b_toa, 0);

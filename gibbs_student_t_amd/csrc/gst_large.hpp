@@ -39,6 +39,10 @@ constexpr int LBLK = 256;      // threads of the per-chain kernels (4 waves)
 constexpr int TBLK = 1024;
 constexpr int TBLK_SMALL = 256;
 constexpr int TBLK_SMALL_NPAD = 32768;
+// lg_white only: one wave per chain up to 8k TOAs (its 21 likelihood passes are then a few
+// loads and one wave reduction each, with no workgroup barrier)
+constexpr int TBLK_WAVE = 64;
+constexpr int TBLK_WAVE_NPAD = 8192;
 constexpr int GRAM_WAVES = 8;  // chains per gram workgroup
 constexpr int TM_PW = 16;      // panel width of the timing-model elimination
 
@@ -100,6 +104,10 @@ __device__ __forceinline__ const double* tape_row(const LArgs& a, int c) {
 // Deterministic block sum (NW waves): every thread gets the bitwise-identical value.
 template <int NW = 4>
 __device__ __forceinline__ double block_sum(double v, double* red) {
+  if constexpr (NW == 1) {   // one wave: no barrier
+    (void)red;
+    return wave_sum(v);
+  }
   v = wave_sum(v);
   const int wv = threadIdx.x >> 6;
   __syncthreads();
@@ -192,14 +200,18 @@ struct WhiteNoise {
   int nb;
   __device__ __forceinline__ double n0(int t) const {
     if (nb <= 1) return ef2[0] * s2[t] + Q[0];
-    const int b = bk[t];
+    return n0v(bk[t], s2[t]);
+  }
+  // N0 of a TOA of backend b (0 with one backend) and sigma^2 sv
+  __device__ __forceinline__ double n0v(int b, double sv) const {
+    if (nb <= 1) return ef2[0] * sv + Q[0];
     double e = ef2[0], q = Q[0];
 #pragma unroll
     for (int j = 1; j < NBMAX; ++j) {
       e = (b == j) ? ef2[j] : e;
       q = (b == j) ? Q[j] : q;
     }
-    return e * s2[t] + q;
+    return e * sv + q;
   }
 };
 
@@ -259,6 +271,7 @@ __global__ void __launch_bounds__(TB) lg_white(const DevModel* __restrict__ mds,
     a.st.status[c] |= 4;                          // bad dataset index (ran on dataset 0)
   __shared__ double red[TB / 64];
   __shared__ double mhv[NWHITE][4];
+  constexpr int WU = TB == 64 ? 8 : 4;   // TOAs per thread per round of the per-TOA loops
   const int n = md.n, nst = a.st.nst, npad = md.npad;
   const double* zc = a.st.z + (size_t)c * nst;
   const double* alc = a.st.alpha + (size_t)c * nst;
@@ -274,12 +287,26 @@ __global__ void __launch_bounds__(TB) lg_white(const DevModel* __restrict__ mds,
 
   if (do_white) {
     // fixed over the block: a_t = alpha_t^z_t, y_t^2 / a_t and sum log a_t
+    // (U TOAs per thread per round, their loads issued first: one load round trip per round,
+    // not per TOA; the TOAs past n in the last round are masked)
     double la = 0.0;
-    for (int t = threadIdx.x; t < n; t += TB) {
-      const bool zt = zc[t] != 0.0;
-      const double at = zt ? alc[t] : 1.0;
-      if (zt) la += log(at);
-      wc[t] = yc[t] * yc[t] / at;
+    for (int t0 = threadIdx.x; t0 < n; t0 += WU * TB) {
+      double zv[WU], av[WU], yw[WU];
+#pragma unroll
+      for (int k = 0; k < WU; ++k) {
+        const int t = t0 + k * TB < n ? t0 + k * TB : (int)threadIdx.x;
+        zv[k] = zc[t];
+        av[k] = alc[t];
+        yw[k] = yc[t];
+      }
+#pragma unroll
+      for (int k = 0; k < WU; ++k) {
+        if (t0 + k * TB >= n) continue;
+        const bool zt = zv[k] != 0.0;
+        const double at = zt ? av[k] : 1.0;
+        if (zt) la += log(at);
+        wc[t0 + k * TB] = yw[k] * yw[k] / at;
+      }
     }
     la = block_sum<TB / 64>(la, red);
     if (!a.eval_only && threadIdx.x < NWHITE) mh_variate(md, rng, tp, threadIdx.x, mhv[threadIdx.x]);
@@ -296,25 +323,24 @@ __global__ void __launch_bounds__(TB) lg_white(const DevModel* __restrict__ mds,
         const double e = wn.ef2[0], q = wn.Q[0];
         const GDouble* s2 = (const GDouble*)wn.s2;
         const GDouble* w2 = (const GDouble*)wc;
-        int t = threadIdx.x;
-        for (; t + 3 * TB < n; t += 4 * TB) {
-          double sv[4], wv[4];
+        // WU TOAs per thread per round, all loads issued first; the last round's TOAs past
+        // n are masked (they read TOA threadIdx.x and contribute factor 1 / term 0)
+        constexpr int U = WU;
+        for (int t0 = threadIdx.x; t0 < n; t0 += U * TB) {
+          double sv[U], wv[U];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            sv[k] = s2[t + k * TB];
-            wv[k] = w2[t + k * TB];
+          for (int k = 0; k < U; ++k) {
+            const int t = t0 + k * TB < n ? t0 + k * TB : (int)threadIdx.x;
+            sv[k] = s2[t];
+            wv[k] = w2[t];
           }
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
+          for (int k = 0; k < U; ++k) {
+            const bool in = t0 + k * TB < n;
             const double N0 = e * sv[k] + q;
-            lp.mul(N0);
-            sq += div_pos(wv[k], N0);
+            lp.mul(in ? N0 : 1.0);
+            sq += in ? div_pos(wv[k], N0) : 0.0;
           }
-        }
-        for (; t < n; t += TB) {
-          const double N0 = e * s2[t] + q;
-          lp.mul(N0);
-          sq += div_pos(w2[t], N0);
         }
       } else {
         for (int t = threadIdx.x; t < n; t += TB) {
@@ -358,15 +384,31 @@ __global__ void __launch_bounds__(TB) lg_white(const DevModel* __restrict__ mds,
   const WhiteNoise wf = white_noise(md, xv);
   double sr = 0.0;
   LogProd lp;
-  for (int t = threadIdx.x; t < npad; t += TB) {
-    double wt = 0.0;
-    if (t < n) {
-      const double N = (zc[t] != 0.0 ? alc[t] : 1.0) * wf.n0(t);
-      lp.mul(N);
-      sr += md.resid[t] * md.resid[t] / N;
-      wt = 1.0 / N;
+  for (int t0 = threadIdx.x; t0 < npad; t0 += WU * TB) {
+    double zv[WU], av[WU], sv[WU], rv[WU];
+    int bv[WU];
+#pragma unroll
+    for (int k = 0; k < WU; ++k) {
+      const int t = t0 + k * TB < n ? t0 + k * TB : (int)threadIdx.x;
+      zv[k] = zc[t];
+      av[k] = alc[t];
+      sv[k] = wf.s2[t];
+      rv[k] = md.resid[t];
+      bv[k] = wf.nb > 1 ? wf.bk[t] : 0;
     }
-    wc[t] = wt;
+#pragma unroll
+    for (int k = 0; k < WU; ++k) {
+      const int t = t0 + k * TB;
+      if (t >= npad) continue;
+      double wt = 0.0;
+      if (t < n) {
+        const double N = (zv[k] != 0.0 ? av[k] : 1.0) * wf.n0v(bv[k], sv[k]);
+        lp.mul(N);
+        sr += rv[k] * rv[k] / N;
+        wt = 1.0 / N;
+      }
+      wc[t] = wt;
+    }
   }
   const double sl = block_sum<TB / 64>(lp.log_sum(), red);
   sr = block_sum<TB / 64>(sr, red);
