@@ -20,6 +20,8 @@ STAGE_GRAM = 0x100          # timing diagnostic: Gram + timing-model elimination
 TAPE_WHITE, TAPE_HYPER, TAPE_DELTA = 0, 80, 120
 PATH_AUTO, PATH_PERSISTENT, PATH_LARGE = 0, 1, 2
 DEBUG_POISON = 1
+DEBUG_LARGE_GRAM = 2
+DEBUG_LARGE_HYPER = 4
 PATHS = {"auto": PATH_AUTO, "persistent": PATH_PERSISTENT, "large": PATH_LARGE}
 KERNEL_KINDS = ("record", "white", "gram", "tmelim", "hyper", "btm", "tb", "toa")
 

@@ -588,14 +588,14 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
   const int npairs = nsb * (nsb + 1) / 2;
   const bool small_toa = ys <= gst::TBLK_SMALL_NPAD;
   // hyper blocks of up to HR_COLS (62) columns: one wave per chain, register-resident elimination
-  bool hyper_reg = true;
+  bool hyper_reg = !(cx->debug & GST_DEBUG_LARGE_HYPER);
   for (const gst::DevModel& hm : cx->hmd) hyper_reg = hyper_reg && hm.nf + hm.nec <= gst::HR_COLS;
   const dim3 g_hr((C + gst::HR_WPB - 1) / gst::HR_WPB), b_hr(64 * gst::HR_WPB);
   // Grams of at most GS_NTMAX 16-column tiles: one wave per chain (lg_gram_small<NT>)
   int gram_small = h.mp / 16;
   for (const gst::DevModel& hm : cx->hmd)
     if (hm.mp != h.mp) gram_small = 0;
-  if (gram_small > gst::GS_NTMAX) gram_small = 0;
+  if (gram_small > gst::GS_NTMAX || (cx->debug & GST_DEBUG_LARGE_GRAM)) gram_small = 0;
   const dim3 g_gs((C + gst::GS_WPB - 1) / gst::GS_WPB), b_gs(64 * gst::GS_WPB);
   const dim3 g_chain(C), b_chain(gst::LBLK), b_toa(small_toa ? gst::TBLK_SMALL : gst::TBLK);
   const dim3 g_gram(npairs * ((C + gst::GRAM_WAVES - 1) / gst::GRAM_WAVES)), b_gram(64 * gst::GRAM_WAVES);
@@ -775,7 +775,8 @@ int gst_set_waves(void* ctx, int waves) {
 int gst_set_debug(void* ctx, int flags) {
   Ctx* cx = static_cast<Ctx*>(ctx);
   if (!cx) return fail("gst_set_debug: null ctx");
-  if (flags & ~GST_DEBUG_POISON) return fail("gst_set_debug: unknown flag");
+  if (flags & ~(GST_DEBUG_POISON | GST_DEBUG_LARGE_GRAM | GST_DEBUG_LARGE_HYPER))
+    return fail("gst_set_debug: unknown flag");
   cx->debug = flags;
   return 0;
 }

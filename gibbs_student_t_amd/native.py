@@ -156,10 +156,14 @@ class NativeSampler:
         code = {"auto": 0, 1: 1, 2: 2}[waves]
         _abi.check(self.lib, self.lib.gst_set_waves(self.ctx, code), "gst_set_waves")
 
-    def set_debug(self, poison: bool = False):
+    def set_debug(self, poison: bool = False, large_gram: bool = False,
+                  large_hyper: bool = False):
         """gst_set_debug: GST_DEBUG_POISON overwrites every chain's LDS and parked scratch
-        with NaN at each sweep start (a check that no sweep reads stale state)."""
-        flags = _abi.DEBUG_POISON if poison else 0
+        with NaN at each sweep start (a check that no sweep reads stale state);
+        GST_DEBUG_LARGE_GRAM / _HYPER force the large path's generic Gram / hyper kernels
+        (tests compare them with the mid-size kernels)."""
+        flags = ((_abi.DEBUG_POISON if poison else 0) | (_abi.DEBUG_LARGE_GRAM if large_gram else 0)
+                 | (_abi.DEBUG_LARGE_HYPER if large_hyper else 0))
         _abi.check(self.lib, self.lib.gst_set_debug(self.ctx, flags), "gst_set_debug")
 
     # ---- state ---------------------------------------------------------------------

@@ -225,7 +225,12 @@ int gst_set_waves(void* ctx, int waves);
  * pattern; since a chain carries no state between sweeps beyond its state arrays, a launch
  * with this flag must give bitwise the same chains as one without (a read of any stale word
  * would surface as NaN / different draws).  Costs time; never set in production. */
-enum gst_debug { GST_DEBUG_POISON = 1 };
+/* Large path: GST_DEBUG_LARGE_GRAM forces the 64x64 super-tile Gram (lg_gram) where the
+ * one-wave-per-chain Gram (lg_gram_small) would run; the two give bitwise the same G.
+ * GST_DEBUG_LARGE_HYPER forces the LDS-resident hyper kernel (lg_hyper) where the register-
+ * resident one (lg_hyper_reg) would run: same variates and decisions, likelihoods within
+ * rounding.  Test switches (the defaults are the faster kernels). */
+enum gst_debug { GST_DEBUG_POISON = 1, GST_DEBUG_LARGE_GRAM = 2, GST_DEBUG_LARGE_HYPER = 4 };
 int gst_set_debug(void* ctx, int flags);
 
 /* Per-kernel timing of the large path (HIP events around every launch of the next

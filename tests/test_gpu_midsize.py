@@ -1,0 +1,75 @@
+"""Mid-size pulsars on the large path: the one-wave-per-chain kernels against the
+generic ones they replace, at a size the persistent kernel does not take (n = 1000).
+
+* lg_gram_small must give bitwise lg_gram's Gram: whole chains are compared bitwise with the
+  generic Gram forced (GST_DEBUG_LARGE_GRAM).
+* lg_hyper_reg runs the same MH with another elimination: likelihoods within rounding, the
+  same discrete draws, continuous draws within 1e-8 (GST_DEBUG_LARGE_HYPER).
+
+The kernels' parity with the reference itself is covered by the large-path replays of
+test_gpu_parity.py, whose fixtures (m = 74) run on these same kernels.
+"""
+import numpy as np
+import pytest
+
+from gibbs_student_t_amd import data
+from gibbs_student_t_amd.model import PTA
+from gibbs_student_t_amd.native import NativeSampler
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+CFG = dict(model="mixture", vary_df=True, theta_prior="beta")
+C, S = 16, 6
+
+
+@pytest.fixture(scope="module")
+def pta():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    return PTA(data.scaled_synthetic(n=1000, components=30, ntm=14, seed=11), components=30)
+
+
+def _run(pta, **debug):
+    ns = NativeSampler(pta, CFG, 0)
+    assert ns.path == "large"
+    ns.set_debug(**debug)
+    ns.alloc(C)
+    rng = np.random.default_rng(5)
+    lo = np.array([p.pmin for p in pta.params])
+    hi = np.array([p.pmax for p in pta.params])
+    x0 = rng.uniform(lo, hi, size=(C, len(lo)))
+    ns.set_state(x=x0, z=np.zeros((C, ns.n)), alpha=np.ones((C, ns.n)),
+                 theta=np.full(C, 0.05), nu=np.full(C, 4.0))
+    lnl = ns.eval_lnlike()
+    rec = ns.alloc_records(S)
+    ns.sweep(S, records=rec, seed=21)
+    out = {k: v.cpu().numpy() for k, v in rec.items()}
+    out["status"] = ns.get_state()["status"]
+    ns.close()
+    return lnl, out
+
+
+def test_small_gram_is_bitwise_the_supertile_gram(pta):
+    lnl_a, a = _run(pta)
+    lnl_b, b = _run(pta, large_gram=True)
+    assert np.all(a["status"] == 0) and np.all(b["status"] == 0)
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    for u, v in zip(lnl_a, lnl_b):
+        np.testing.assert_array_equal(np.asarray(u), np.asarray(v))
+
+
+def test_register_hyper_matches_lds_hyper(pta):
+    lnl_a, a = _run(pta)
+    lnl_b, b = _run(pta, large_hyper=True)
+    assert np.all(a["status"] == 0) and np.all(b["status"] == 0)
+    # white lnL: same kernel; hyper (b-marginalised) lnL: two eliminations of one matrix
+    np.testing.assert_array_equal(np.asarray(lnl_a[0]), np.asarray(lnl_b[0]))
+    h_a, h_b = np.asarray(lnl_a[1]), np.asarray(lnl_b[1])
+    assert np.all(np.abs(h_a - h_b) <= 1e-11 * np.abs(h_b)), np.max(np.abs(h_a - h_b) / np.abs(h_b))
+    for k in ("x", "z", "nu"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    for k in ("b", "alpha", "pout", "theta"):
+        d = np.abs(a[k] - b[k])
+        assert np.all(d <= 1e-8 * np.maximum(np.abs(b[k]), 1e-300) + 1e-300), (k, d.max())
