@@ -447,8 +447,11 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
   const int MT = sh ? sh->MT : 0, K0 = sh ? sh->K0 : 0;
   const int raug = sh ? sh->RA : 0;
   const int nsl = (nmax + 63) / 64;
-  // TOA slots of 64 held in registers: 2, 3, 4 (J1713-sized), 6, 8 (mid-size, n <= 512)
-  const int NS = nsl <= 2 ? 2 : (nsl <= 3 ? 3 : (nsl <= 4 ? 4 : (nsl <= 6 ? 6 : 8)));
+  // TOA slots of 64 held in registers: 2, 3, 4 (J1713-sized), 6, 8 (mid-size, n <= 512),
+  // 12, 16 (wide mid-size, n <= 1024: the run_sims model's shape only; these keep one chain
+  // per SIMD, their two-chains-per-SIMD builds would spill kilobytes per lane)
+  const int NS = nsl <= 2 ? 2 : (nsl <= 3 ? 3 : (nsl <= 4 ? 4 : (nsl <= 6 ? 6 : (nsl <= 8 ? 8 :
+                 (nsl <= 12 ? 12 : 16)))));
   const bool fits = sh && classic(d) && round_up(nmax, 4) <= 64 * NS &&
                     pick(MT, NS, K0, raug, false, 4, false);
   int path = cx->path_req;
@@ -687,7 +690,8 @@ static int launch(Ctx* cx, const gst_state* s, const gst_records* r, const gst_t
   // two waves per chain when every chain would otherwise leave a SIMD idle
   const bool pair = !tape && !eval_only && !(mask & GST_STAGE_GRAM) &&
                     (cx->waves == GST_WAVES_TWO || (cx->waves == GST_WAVES_AUTO && C <= 2 * cx->ncu));
-  kfn_t k = pick(cx->MT, cx->NS, cx->K0, cx->raug, tape, wpb, C > 4 * cx->ncu, pair);
+  kfn_t k = pick(cx->MT, cx->NS, cx->K0, cx->raug, tape, wpb,
+                 C > 4 * cx->ncu && cx->NS <= gst::OCC2_NS_MAX, pair);
   if (!k) return fail("gst: no kernel instance");
   // timing-model factor scratch: [C][waves per chain][slots with s < K0][64] doubles
   const int ntms = cx->MT * (cx->MT + 1) / 2 - (cx->MT - cx->K0) * (cx->MT - cx->K0 + 1) / 2;

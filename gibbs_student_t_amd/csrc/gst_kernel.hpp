@@ -60,6 +60,9 @@ __host__ __device__ constexpr int SL(int r, int s) { return r * (r + 1) / 2 + s;
 // (pairing earlier spills there, and its second wave already covers much of the hand-off
 // latency).
 constexpr int KP_MIN = 4;
+// the largest TOA-slot count whose two-chains-per-SIMD build the host picks (wider shapes
+// run one chain per SIMD)
+constexpr int OCC2_NS_MAX = 8;
 __host__ __device__ constexpr int pair_pw(int MT) { return MT - KP_MIN; }
 __host__ __device__ constexpr int kp_for(int OCC) { return OCC == 2 ? 6 : KP_MIN; }
 // index of slot (r, s), s < K0, among the timing-model factor slots (column-major)

@@ -22,6 +22,8 @@ typedef void (*kfn_t)(const DevModel*, const DevState, const DevRec, const DevTa
   X(10, 4, 2, 76) /* n <= 256 */                                                   \
   X(10, 6, 2, 76) /* mid-size pulsars: n <= 384 */                                 \
   X(10, 8, 2, 76) /* n <= 512 */                                                   \
+  X(10, 12, 2, 76) /* wide mid-size (round 3): n <= 768, one chain per SIMD only */ \
+  X(10, 16, 2, 76) /* n <= 1024 */                                                 \
   X(8, 2, 2, 56)  /* <= 20 red-noise components, <= 16 TM columns */               \
   X(8, 3, 2, 56)                                                                   \
   X(8, 4, 2, 56)                                                                   \

@@ -1,5 +1,6 @@
 """Mid-size pulsars on the large path: the one-wave-per-chain kernels against the
-generic ones they replace, at a size the persistent kernel does not take (n = 1000).
+generic ones they replace, at n = 1000 (the large path forced: since round 3 the persistent
+kernel's 16-slot instance takes pulsars of up to 1024 TOAs).
 
 * lg_gram_small must give bitwise lg_gram's Gram: whole chains are compared bitwise with the
   generic Gram forced (GST_DEBUG_LARGE_GRAM).
@@ -31,8 +32,7 @@ def pta():
 
 
 def _run(pta, **debug):
-    ns = NativeSampler(pta, CFG, 0)
-    assert ns.path == "large"
+    ns = NativeSampler(pta, CFG, 0, path="large")   # n <= 1024 would pick the persistent kernel
     ns.set_debug(**debug)
     ns.alloc(C)
     rng = np.random.default_rng(5)

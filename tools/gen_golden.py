@@ -426,8 +426,27 @@ def mid(niter=12):
         print("mid", name, "n", pta_m.n, "cond:", np.nanmax(out["tape_b_cond"]), file=sys.stderr)
 
 
+def wide(niter=12):
+    """A wider mid-size pulsar for the register-resident kernel's 16-slot instance (n <= 1024):
+    130 J1713+0747 epochs x 7 sub-band TOAs (gdata.multiband, one backend's labels ignored),
+    n = 910, the classic run_sims model (30 components)."""
+    psr = gdata.multiband(nepochs=130, nsub=7, seed=910)
+    pta_w = PTA(psr)
+    np.savez_compressed(os.path.join(OUTDIR, "wide_dataset.npz"), **dataset_arrays(pta_w, psr))
+    for j, name in enumerate(("beta", "t")):
+        out = run_one(pta_w, name, MODELS[name], seed=9100 + 11 * j, niter=niter,
+                      x0=[4.33, -14.0, -7.6])
+        out["model_kw"] = np.array(repr(MODELS[name]))
+        np.savez_compressed(os.path.join(OUTDIR, f"ref_wide_{name}_fixed.npz"), **out)
+        print("wide", name, "n", pta_w.n, "cond:", np.nanmax(out["tape_b_cond"]),
+              file=sys.stderr)
+
+
 def main():
     os.makedirs(OUTDIR, exist_ok=True)
+    if "--only-wide" in sys.argv:
+        wide(12)
+        return
     if "--only-general" in sys.argv:
         general(12)
         return
@@ -493,6 +512,7 @@ def main():
     shapes(niter)
     general(niter)
     mid(niter)
+    wide(niter)
 
 
 if __name__ == "__main__":

@@ -5,7 +5,8 @@ large-model pipeline for the same model.
     python tools/mid_size.py [chains] [sweeps] [out.json]
 
 Datasets: gdata.multiband epochs (J1713+0747 epochs x sub-band TOAs) under the classic
-run_sims model (30 components, 14 timing-model columns), n = 260 and 390 and 512.
+run_sims model (30 components, 14 timing-model columns), n = 260, 390, 512, 650, 910
+(the last two on the 12- and 16-slot instances, round 3).
 """
 import json
 import sys
@@ -42,7 +43,7 @@ def main():
     S = int(sys.argv[2]) if len(sys.argv) > 2 else 100
     out = {"chains": C, "sweeps": S, "model": "run_sims 'beta', 30 components, 14 TM columns",
            "rows": []}
-    for nepochs, nsub in ((130, 2), (130, 3), (128, 4)):
+    for nepochs, nsub in ((130, 2), (130, 3), (128, 4), (130, 5), (130, 7)):
         psr = data.multiband(nepochs=nepochs, nsub=nsub, seed=7)
         pta = PTA(psr)
         for path in ("persistent", "large"):
