@@ -201,7 +201,8 @@ int gst_sync(void* ctx, void* stream);
 
 /* Execution path.  The persistent path keeps a whole chain in one wavefront for all of a
  * launch's sweeps (n <= 512 and up to 30 red-noise components with <= 16 timing-model
- * columns, 26 with <= 24; smaller models run padded with unit-prior dummy columns); the
+ * columns, 26 with <= 24, n <= 1024 for the 30-component / 16-column shape; smaller models
+ * run padded with unit-prior dummy columns); the
  * large path runs
  * each sweep as a pipeline of kernels (fp64-MFMA Gram shared by all chains, blocked
  * timing-model elimination, LDS-resident red-noise MH, MFMA T b, per-TOA passes) for
