@@ -531,7 +531,9 @@ def main():
             pass
     else:
         from gibbs_student_t_amd.native import NativeSampler as Sampler
-        dev = torch.device("cuda", local)
+        # local % devices: only ever < 1 on a node with fewer GPUs than ranks, i.e. the
+        # gloo rehearsal of several ranks on one GPU (dist.init, GST_DIST_BACKEND)
+        dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
         torch.cuda.set_device(dev)
 
         def sync():
@@ -539,7 +541,7 @@ def main():
     wl = workload(args.config, rank, world, args.chains)
     C, K, W = wl["C"], args.steps, args.warmup
     c0 = wl["chain0"]
-    ns = Sampler(wl["ptas"], wl["cfgs"], local)
+    ns = Sampler(wl["ptas"], wl["cfgs"], dev.index if dev is not None else local)
     ns.alloc(C, dataset=wl["ds"])
     ns.set_state(**wl["init"])
     if W > 0:
@@ -717,7 +719,7 @@ def main():
                        "basis_cols": m, "datasets_per_gpu": len(wl["ptas"]),
                        "record_every": 1,
                        "parallelism": f"independent chains sharded over {world} GPU(s); "
-                                      "RCCL only for the final all-gather of chain draws"},
+                                      "RCCL only for the final gather of chain draws to rank 0"},
             "ess_per_sec": ess_ps,
             "ess_per_sec_reason": reason,
             # config 4: the same per outlier model of the run_sims grid (each model's chains

@@ -24,11 +24,15 @@ def env_rank():
 
 
 def init(backend: str | None = None):
-    """Initialise the process group when launched by torch.distributed.run."""
+    """Initialise the process group when launched by torch.distributed.run.  The backend is
+    RCCL ("nccl") with a GPU, gloo without; ``GST_DIST_BACKEND`` overrides it (gloo ranks
+    sharing one GPU rehearse the multi-rank path on a one-GPU box: RCCL refuses two ranks
+    on one device)."""
     import torch.distributed as dist
     rank, local, world = env_rank()
     if world <= 1 or dist.is_initialized():
         return rank, local, world
+    backend = os.environ.get("GST_DIST_BACKEND") or backend
     if backend is None:
         import torch
         backend = "nccl" if torch.cuda.is_available() else "gloo"
@@ -43,13 +47,22 @@ def chain_range(rank: int, chains_per_rank: int):
     return rank * chains_per_rank, (rank + 1) * chains_per_rank
 
 
+def _coll_device(device):
+    """Where a collective's tensors live: the rank's GPU under RCCL, host memory otherwise."""
+    import torch
+    import torch.distributed as dist
+    if device is not None and dist.get_backend() == "nccl":
+        return device
+    return torch.device("cpu")
+
+
 def reduce_summary(vec_sum: np.ndarray, vec_max: np.ndarray, device=None):
     """All-reduce per-rank summaries: sums (ESS, counts) and maxima (time, R-hat)."""
     import torch
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()):
         return np.asarray(vec_sum, float), np.asarray(vec_max, float)
-    dev = device if device is not None else torch.device("cpu")
+    dev = _coll_device(device)
     s = torch.as_tensor(np.asarray(vec_sum, float), device=dev)
     m = torch.as_tensor(np.asarray(vec_max, float), device=dev)
     dist.all_reduce(s, op=dist.ReduceOp.SUM)
@@ -70,7 +83,7 @@ def gather_chains(arr: np.ndarray, device=None):
     if not (dist.is_available() and dist.is_initialized()):
         return a
     world, rank = dist.get_world_size(), dist.get_rank()
-    dev = device if device is not None else torch.device("cpu")
+    dev = _coll_device(device)
     t = torch.as_tensor(a, device=dev)
     parts = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
     dist.gather(t, gather_list=parts, dst=0)
