@@ -152,8 +152,8 @@ constexpr int TP_WHITE = 0, TP_HYPER = 80, TP_DELTA = 120;
 // loads; the 8 owner lanes (q == column residue) write it.  Row stride MT = 10 doubles puts
 // the 8 p-rows of a 128-bit read in distinct bank groups (80 B apart).
 
-// diagnostic builds: slots 0-15 and 19 cycle sums (tools/stage_profile.py), 16-18 event counts
-constexpr int GST_NSTAMP = 20;
+// diagnostic builds: slots 0-15, 19-23 cycle sums (tools/stage_profile.py), 16-18 event counts
+constexpr int GST_NSTAMP = 24;
 #ifdef GST_STAMPS
 #define GST_STAMP_DECL \
   unsigned long long st_acc[GST_NSTAMP] = {0}, st_t0 = 0, st_s0 = 0;
@@ -1536,7 +1536,9 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     }
 
     const double x_last0 = pget(xv, P - 1);  // chain[ii, -1]
+    GST_SUB_BEGIN
     if (!eval_only) mh_variates(tp);
+    GST_SUB_END(20)
     GST_STAMP(0)
 
     // ---- white-noise MH block (gibbs.py:114-143); step -1 = the initial lnlike0
@@ -1547,7 +1549,9 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       // accept/reject path b (bit i = step s0+i accepted); the decisions are then read
       // back lane by lane.  Every value is computed with the sequential code's exact
       // operation order, so the decisions and the final state are bitwise identical.
+      GST_SUB_BEGIN
       white_prep();
+      GST_SUB_END(21)
       constexpr int D = 6;
       double Wu[8];
 #pragma unroll
@@ -1569,61 +1573,81 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         }
         return -0.5 * ((sl + wcls_la) + sq);
       };
-      double Qx = exp(2.0 * pget(xv, md.idx_equad) * 2.302585092994045684);
+      const int ieq = md.idx_equad;
+      double Qx = exp(2.0 * pget(xv, ieq) * 2.302585092994045684);
       double l0 = lnl_lane(xv, Qx), p0 = lnprior(xv);
+      // this lane's node: level j, path b
+      const int node = lane + 1;
+      const int j = 31 - __builtin_clz(node);          // node in [2^j, 2^(j+1))
+      const int b = node - (1 << j);
 #pragma unroll 1
       for (int s0 = 0; s0 < NWHITE; s0 += D) {
         const int nd = (NWHITE - s0) < D ? (NWHITE - s0) : D;
-        // this lane's node: level j, path b
-        const int node = lane + 1;
-        const int j = 31 - __builtin_clz(node);          // node in [2^j, 2^(j+1))
-        const int b = node - (1 << j);
+        GST_SUB_BEGIN
+        // the round's D steps (parameter, delta, log u, 10^(2 delta)) in registers: every
+        // LDS load issues up front, and each lane's walk down its path is straight-line
+        // selects instead of a divergent loop of dependent loads
+        int pr[D];
+        double dl[D], lu[D], ev[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+          const int gs = (s0 + i) < NWHITE ? s0 + i : NWHITE - 1;
+          pr[i] = (int)mhw[4 * gs + 0];
+          dl[i] = mhw[4 * gs + 1];
+          lu[i] = mhw[4 * gs + 2];
+          ev[i] = mhw[4 * gs + 3];
+        }
         double xq[4], Q = Qx;
 #pragma unroll
         for (int t = 0; t < 4; ++t) xq[t] = xv[t];
+#pragma unroll
+        for (int i = 0; i < D - 1; ++i) {
+          const bool on = i < j && ((b >> i) & 1);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) xq[t] = (on && t == pr[i]) ? xq[t] + dl[i] : xq[t];
+          Q = (on && pr[i] == ieq) ? Q * ev[i] : Q;
+        }
+        // the proposal of step s0 + j from the node's state (propose(): q[par] += delta)
+        int par = pr[0];
+        double delta = dl[0], E = ev[0];
+#pragma unroll
+        for (int i = 1; i < D; ++i) {
+          par = j == i ? pr[i] : par;
+          delta = j == i ? dl[i] : delta;
+          E = j == i ? ev[i] : E;
+        }
+        double qv[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) qv[t] = (t == par) ? xq[t] + delta : xq[t];
         double p1 = -INFINITY, l1 = 0.0;
         if (j < nd) {
-          for (int i = 0; i < j; ++i) {
-            if ((b >> i) & 1) {
-              const int gs = s0 + i;
-              const int par = (int)mhw[4 * gs + 0];
-              const double delta = mhw[4 * gs + 1];
-#pragma unroll
-              for (int t = 0; t < 4; ++t) xq[t] = (t == par) ? xq[t] + delta : xq[t];
-              if (par == md.idx_equad) Q = Q * mhw[4 * gs + 3];
-            }
-          }
-          double qv[4], E;
-          int par;
-          (void)propose(xq, qv, s0 + j, E, par);
-          const double Qq = (par == md.idx_equad) ? Q * E : Q;
+          const double Qq = (par == ieq) ? Q * E : Q;
           p1 = lnprior(qv);
           if (p1 != -INFINITY) l1 = lnl_lane(qv, Qq);
         }
-        GST_SUB_BEGIN
+        GST_SUB_END(22)
         int path = 0;
-        for (int jj = 0; jj < nd; ++jj) {
-          const int L = (1 << jj) - 1 + path;
-          const double pl = rdlane(p1, L);
-          const double ll = rdlane(l1, L);
-          const double luacc = mhw[4 * (s0 + jj) + 2];
-          if (pl != -INFINITY && (ll + pl) - (l0 + p0) > luacc) {
-            l0 = ll;
-            p0 = pl;
-            path |= 1 << jj;
+#pragma unroll
+        for (int jj = 0; jj < D; ++jj) {
+          if (jj < nd) {
+            const int L = (1 << jj) - 1 + path;
+            const double pl = rdlane(p1, L);
+            const double ll = rdlane(l1, L);
+            if (pl != -INFINITY && (ll + pl) - (l0 + p0) > lu[jj]) {
+              l0 = ll;
+              p0 = pl;
+              path |= 1 << jj;
+            }
           }
         }
         GST_SUB_END(15)
         // apply the accepted moves in order (the sequential code's xv = qv, Qx = Qq)
-        for (int i = 0; i < nd; ++i) {
-          if ((path >> i) & 1) {
-            const int gs = s0 + i;
-            const int par = (int)mhw[4 * gs + 0];
-            const double delta = mhw[4 * gs + 1];
 #pragma unroll
-            for (int t = 0; t < 4; ++t) xv[t] = (t == par) ? xv[t] + delta : xv[t];
-            if (par == md.idx_equad) Qx = Qx * mhw[4 * gs + 3];
-          }
+        for (int i = 0; i < D; ++i) {
+          const bool on = i < nd && ((path >> i) & 1);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) xv[t] = (on && t == pr[i]) ? xv[t] + dl[i] : xv[t];
+          Qx = (on && pr[i] == ieq) ? Qx * ev[i] : Qx;
         }
       }
     } else if ((mask & 1u) || eval_only) {

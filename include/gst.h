@@ -245,9 +245,9 @@ int gst_set_timing(void* ctx, int on);
 int gst_kernel_times(void* ctx, double* ms, int* launches, int nkinds);
 
 /* Diagnostic builds (-DGST_STAMPS) only: per-chain per-stage s_memtime cycle sums (slots
- * 0-15 and 19) and event counts (16: red-noise likelihoods, 17: two-wave rounds, 18: accepted
- * red-noise proposals) are accumulated into dev_buf[C][20]; returns an error in production
- * builds. */
+ * 0-15 and 19-23) and event counts (16: red-noise likelihoods, 17: two-wave rounds, 18:
+ * accepted red-noise proposals) are accumulated into dev_buf[C][24]; returns an error in
+ * production builds. */
 int gst_debug_stamps(void* ctx, unsigned long long* dev_buf);
 
 /* Kernel-level timing of the last gst_sweep on its stream (hipEvents), milliseconds. */
