@@ -194,9 +194,9 @@ def workload(config: int, rank: int, world: int, chains: int | None):
         e0 = rank * per_rank
         mine = grid[e0:e0 + per_rank]
         nst = max(e.pta.n for e in mine)
-        # vvh17 entries start as run_sims.Study does by default (z = 0: the reference's z = 1
-        # start is left only after ~1000-5000 sweeps with the exact b draw)
-        parts = [run_sims.initial_state(e, per_entry, (e0 + i) * per_entry, 7, nst, "clean")
+        # every entry starts as gibbs.py:29-51 does (vvh17: z = 1, left through the b draw's
+        # SVD noise floor as the reference's chains leave it)
+        parts = [run_sims.initial_state(e, per_entry, (e0 + i) * per_entry, 7, nst, "reference")
                  for i, e in enumerate(mine)]
         init = {k: np.concatenate([p_[k] for p_ in parts]) for k in parts[0]}
         C = len(mine) * per_entry
@@ -604,7 +604,8 @@ def main():
         stage_ms = stage_costs(ns, max(1, min(K, 200)), args.seed, W + K + burn + ess_win, c0)
     shards = dist.gather_chains(np.array([[c0, c0 + C]], dtype=np.float64), dev)
     m_vec = np.array([elapsed, kernel_ms, win_s])
-    s_vec = np.array([float((status != 0).sum())])
+    # status bit 4 (16) is informational: a b draw at the SVD noise floor (include/gst.h)
+    s_vec = np.array([float(((status & ~16) != 0).sum()), float(((status & 16) != 0).sum())])
     s_vec, m_vec = dist.reduce_summary(s_vec, m_vec, dev)
     elapsed, kernel_ms, win_s = (float(v) for v in m_vec)
 
@@ -732,6 +733,7 @@ def main():
                            "ess_total": ess, "rhat_max": rhat},
             "shards": [[int(a), int(b)] for a, b in shards],   # global chain ids per rank
             "chains_with_status": int(s_vec[0]),
+            "chains_floor_draw": int(s_vec[1]),
             "kernel_ms": kernel_ms,
             # the persistent kernel is bound by VALU issue and the latency of the
             # factorisations' step-to-step LDS hand-offs (PMC: MFMA busy ~11%, VALU ~57% of

@@ -22,10 +22,12 @@ PATH_AUTO, PATH_PERSISTENT, PATH_LARGE = 0, 1, 2
 DEBUG_POISON = 1
 DEBUG_LARGE_GRAM = 2
 DEBUG_LARGE_HYPER = 4
+DEBUG_EXACT_BDRAW = 8
+STATUS_FLOOR = 16          # status bit 4: a b draw ran at the SVD noise floor
 PATHS = {"auto": PATH_AUTO, "persistent": PATH_PERSISTENT, "large": PATH_LARGE}
 KERNEL_KINDS = ("record", "white", "gram", "tmelim", "hyper", "btm", "tb", "toa")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 EXPORTS = ("gst_version", "gst_tape_stride", "gst_last_error", "gst_ctx_create",
            "gst_ctx_destroy", "gst_model_set", "gst_model_set_batch", "gst_model_info",
            "gst_sweep", "gst_set_path", "gst_get_path", "gst_set_waves", "gst_set_debug", "gst_set_timing", "gst_kernel_times", "gst_eval_lnlike", "gst_sync",

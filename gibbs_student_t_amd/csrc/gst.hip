@@ -66,7 +66,7 @@ struct Ctx {
 // (hipMallocAsync / hipFreeAsync on the launch's stream): no device synchronisation inside
 // gst_sweep, and a buffer is released only after the work queued before it on that stream.
 void free_scratch(Ctx* cx, hipStream_t st) {
-  for (double* p : {cx->ls.G, cx->ls.y, cx->ls.w, cx->ls.sc, cx->ls.v})
+  for (double* p : {cx->ls.G, cx->ls.G2, cx->ls.y, cx->ls.w, cx->ls.sc, cx->ls.v})
     if (p) (void)hipFreeAsync(p, st);
   cx->ls = gst::LScratch{};
   cx->scratch_C = 0;
@@ -566,11 +566,14 @@ static int ensure_scratch(Ctx* cx, int C, hipStream_t st) {
   const gst::DevModel& h = cx->hmd[0];
   const size_t mp = h.mp, npad = large_ys(cx);
   HIP_OK(hipMallocAsync((void**)&cx->ls.G, (size_t)C * mp * mp * 8, st));
+  HIP_OK(hipMallocAsync((void**)&cx->ls.G2, (size_t)C * mp * mp * 8, st));
   HIP_OK(hipMallocAsync((void**)&cx->ls.y, (size_t)C * npad * 8, st));
   HIP_OK(hipMallocAsync((void**)&cx->ls.w, (size_t)C * npad * 8, st));
   HIP_OK(hipMallocAsync((void**)&cx->ls.sc, (size_t)C * 16 * 8, st));
   HIP_OK(hipMallocAsync((void**)&cx->ls.v, (size_t)C * mp * 8, st));
   HIP_OK(hipMemsetAsync(cx->ls.G, 0, (size_t)C * mp * mp * 8, st));
+  HIP_OK(hipMemsetAsync(cx->ls.G2, 0, (size_t)C * mp * mp * 8, st));
+  HIP_OK(hipMemsetAsync(cx->ls.sc, 0, (size_t)C * 16 * 8, st));
   HIP_OK(hipMemsetAsync(cx->ls.v, 0, (size_t)C * mp * 8, st));
   cx->scratch_C = C;
   return 0;
@@ -639,6 +642,18 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
         else
           LG_LAUNCH(GST_K_HYPER, gst::lg_hyper, g_chain, b_chain, cx->lds_hyper);
         if (eval_only) break;
+        if ((mask & 4u) && !(cx->debug & GST_DEBUG_EXACT_BDRAW)) {
+          // the b draw's floor pass (include/gst.h gst_sweep): chains whose Sigma is beyond
+          // fp64 resolution re-eliminate G with Sigma + f I and draw there; every other chain
+          // returns at once (SC_FLOOR == 0)
+          a.floor_pass = 1;
+          LG_LAUNCH(GST_K_TMELIM, gst::lg_tmelim, g_chain, b_chain, cx->lds_tm);
+          if (hyper_reg)
+            LG_LAUNCH(GST_K_HYPER, gst::lg_hyper_reg, g_hr, b_hr, 0);
+          else
+            LG_LAUNCH(GST_K_HYPER, gst::lg_hyper, g_chain, b_chain, cx->lds_hyper);
+          a.floor_pass = 0;
+        }
         if (mask & 4u) {
           LG_LAUNCH(GST_K_BTM, gst::lg_btm, g_chain, b_chain, cx->lds_btm);
           LG_LAUNCH(GST_K_TB, gst::lg_tb, g_tb, b_chain, 0);
@@ -779,7 +794,8 @@ int gst_set_waves(void* ctx, int waves) {
 int gst_set_debug(void* ctx, int flags) {
   Ctx* cx = static_cast<Ctx*>(ctx);
   if (!cx) return fail("gst_set_debug: null ctx");
-  if (flags & ~(GST_DEBUG_POISON | GST_DEBUG_LARGE_GRAM | GST_DEBUG_LARGE_HYPER))
+  if (flags & ~(GST_DEBUG_POISON | GST_DEBUG_LARGE_GRAM | GST_DEBUG_LARGE_HYPER |
+                GST_DEBUG_EXACT_BDRAW))
     return fail("gst_set_debug: unknown flag");
   cx->debug = flags;
   return 0;

@@ -277,6 +277,47 @@ __device__ __forceinline__ double wave_max(double v) {
   return fmax(fmax(rdlane(v, 0), rdlane(v, 16)), fmax(rdlane(v, 32), rdlane(v, 48)));
 }
 
+// ---- SVD noise floor of the b draw (include/gst.h gst_sweep; oracle Oracle.floor_shift) ----
+// The reference draws b through sl.svd(Sigma) (gibbs.py:169-171).  When Sigma's smallest
+// eigenvalues lie below ~eps ||Sigma|| (vvh17's all-outlier start, alpha = 1e10: cond ~ 1e22,
+// while Sigma diagonally scaled is well conditioned) LAPACK returns them at its own rounding
+// floor, ~0.1-6 x 2^-52 s_max, so its draw is in effect one from Sigma + f I -- which is what
+// lets the reference's chains leave that state within ~100 sweeps (the exact draw stays there
+// for thousands).  The b draw reproduces it: when the smallest pivot of
+// the factor over the real columns is below FLOOR_GATE x the largest, b is drawn exactly from
+// Sigma + f I with f = FLOOR_C 2^-52 x the largest pivot; every other draw is the exact one.
+constexpr double FLOOR_GATE = 1e-14;
+constexpr double FLOOR_C = 0.5;
+constexpr int STATUS_FLOOR = 16;
+constexpr int DEBUG_EXACT_BDRAW = 8;
+
+// Smallest / largest pivot over the real columns of a factor whose pivot of internal column
+// j = 64 sl + lane is apr[sl]; real columns are [0, ntm) and [f0, f1) (the rest are unit-prior
+// pads).  Wave-uniform.
+__device__ __forceinline__ void pivot_range(const double (&apr)[2], int lane, int ntm, int f0,
+                                            int f1, double& mn, double& mx) {
+  mx = 0.0;
+  mn = INFINITY;
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) {
+    const int j = 64 * sl + lane;
+    const bool real = j < ntm || (j >= f0 && j < f1);
+    mx = real ? fmax(mx, apr[sl]) : mx;
+    mn = real ? fmin(mn, apr[sl]) : mn;
+  }
+  mx = wave_max(mx);
+  mn = -wave_max(-mn);
+}
+__device__ __forceinline__ double floor_of(double mn, double mx) {
+  return mn < FLOOR_GATE * mx ? FLOOR_C * 0x1p-52 * mx : 0.0;
+}
+__device__ __forceinline__ double floor_shift(const double (&apr)[2], int lane, int ntm, int f0,
+                                              int f1) {
+  double mn, mx;
+  pivot_range(apr, lane, ntm, f0, f1, mn, mx);
+  return floor_of(mn, mx);
+}
+
 // Sum over p (lane bits 3..5) of the lanes with q == qq (lane = 8p + q), uniform result.
 __device__ __forceinline__ double col_sum(double v, int qq) {
   v += dpp<DPP_ROR8>(v);  // (l + 8) mod 16 == l ^ 8
@@ -920,6 +961,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   __shared__ double smem[WPB][lds_doubles(MT, K0)];
   __shared__ double xchg[PAIR ? 2 : 1][2][2];  // pair mode: [round parity][wave] {lnL, failed}
   __shared__ int xdrew[PAIR ? 1 : 1];          // pair mode: the b draw happened this sweep
+  __shared__ double xfloor[1];                 // pair mode: the owner's floor_shift
 
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1186,6 +1228,8 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   double f_apr[2] = {1.0, 1.0}, f_zr[2] = {0.0, 0.0};  // last factorisation's
   int ld_tm_e = 0, fail_tm = 0;
 
+  // SVD noise floor f of this sweep's b draw (floor_shift; 0 except on the floor redo)
+  double fshift = 0.0;
   // Gram: G = T_aug^T diag(1/N) T_aug on fp64 MFMA, then TM elimination -> S0.
   auto gram_and_tm = [&](const double (&xq)[4]) __attribute__((always_inline)) {
     const double ef2 = efac2_of(xq);
@@ -1391,7 +1435,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
 #pragma unroll
     for (int s = 0; s < K0; ++s) {
       const int j = 8 * s + q;
-      if (p == q) L[SL(s, s)] = (j < md.ntm) ? L[SL(s, s)] + md.tm_phiinv : 1.0;
+      if (p == q) L[SL(s, s)] = (j < md.ntm) ? (L[SL(s, s)] + md.tm_phiinv) + fshift : 1.0;
     }
     CholCtx cc{colq, phbuf, colq2, lane, p, q, raug, 1.0, 0.0, 0, 0, {1.0, 1.0}, {0.0, 0.0}};
     GST_SUB_END(10)
@@ -1440,7 +1484,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     // Fourier columns, then the unit-prior dummies that pad a smaller model up to this
     // instance's RA (zero Gram rows: each is eliminated as an exact no-op)
     if (lane < RA - md.ntm_pad)
-      phbuf[md.ntm_pad + lane] = f_live ? exp(-(lc - g * lfreq_l + ldf_l)) : 1.0;
+      phbuf[md.ntm_pad + lane] = f_live ? exp(-(lc - g * lfreq_l + ldf_l)) + fshift : 1.0;
     // phbuf doubles as the eliminations' junk rows: restore the one other entry read
     // below, the augmented row's (no prior on the residual column)
     if (lane == 63) phbuf[raug] = 0.0;
@@ -1701,9 +1745,6 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     int owner = 0;   // the wave whose registers hold the factor at the final x (pair mode)
     if constexpr (PAIR) {
       if (mask & 6u) {
-        gram_and_tm(xv);   // both waves: identical S0 in each wave's own LDS region
-        if (fail_tm) status |= 1;
-        GST_STAMP(2)
         double l0 = 0.0, p0 = 0.0;
         owner = -1;
         bool init = (mask & 2u) != 0;
@@ -1740,6 +1781,12 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
           ++hrej;
           return false;
         };
+        // pass 1 (rare): the b draw's factor at the SVD noise floor, Sigma + f I (floor_shift)
+#pragma unroll 1
+        for (int pass = 0; pass < 2; ++pass) {
+        gram_and_tm(xv);   // both waves: identical S0 in each wave's own LDS region
+        if (fail_tm) status |= 1;
+        GST_STAMP(2)
         // Each round wave 0 evaluates the next point the sequential sampler needs (the
         // initial x, then the next in-prior proposal sa) and wave 1 a speculative one: the
         // step after sa on the branch (accept / reject) the chain's acceptance history
@@ -1837,6 +1884,21 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
             }
           }
         }
+        if (pass == 1 || !redraw || fb || (st.debug & DEBUG_EXACT_BDRAW)) break;
+        // the owner wave holds the factor at the final x; both waves take its floor decision
+        const double fs =
+            role == owner ? floor_shift(f_apr, lane, md.ntm, md.ntm_pad, md.ntm_pad + md.nf) : 0.0;
+        if (role == owner && lane == 0) xfloor[0] = fs;
+        __syncthreads();
+        fshift = xfloor[0];
+        __syncthreads();
+        if (fshift == 0.0) break;
+        status |= STATUS_FLOOR;
+        owner = -1;   // a final round refactors x (the MH decisions stand)
+        init = false;
+        j = NHYPER;
+        }
+        fshift = 0.0;
       }
     } else if ((mask & (6u | 256u)) || eval_only) {
       gram_and_tm(xv);
@@ -1904,6 +1966,19 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     GST_STAMP(3)
 
     bool drew = false;
+    if constexpr (!PAIR) {
+      // the registers hold the factor at the final x: is Sigma beyond fp64 resolution?  Then
+      // refactor x's Sigma + f I (Gram stage + hyper block; the MH decisions stand)
+      if (redraw && !fb && !(st.debug & DEBUG_EXACT_BDRAW)) {
+        fshift = floor_shift(f_apr, lane, md.ntm, md.ntm_pad, md.ntm_pad + md.nf);
+        if (fshift != 0.0) {
+          status |= STATUS_FLOOR;
+          gram_and_tm(xv);
+          lnl_hyper(xv, fb);
+          fshift = 0.0;
+        }
+      }
+    }
     if (redraw && role == owner) {
       if (fb) {
         status |= 2;

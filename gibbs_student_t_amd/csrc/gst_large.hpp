@@ -34,8 +34,10 @@ constexpr int LBLK = 256;      // threads of the per-chain kernels (4 waves)
 // threads per chain of the per-TOA passes (lg_white, lg_toa): 16 waves per chain for the
 // 100k-TOA datasets; 4 for datasets of up to TBLK_SMALL_NPAD TOAs, where a pass is a few
 // TOAs per thread and a 16-wave chain spent it in barriers and reductions with one chain per
-// CU.  Chosen from the datasets alone (never from the chain count), so the chains do not
-// depend on how a launch is sharded.
+// CU.  Chosen from the largest npad of the launch's datasets (never from the chain count):
+// splitting one dataset's chains across launches or ranks does not change them, but the block
+// size sets the reduction order, so a dataset batched with a larger one (> 8k / > 32k TOAs)
+// gives different (equally valid) chains than the same dataset launched alone.
 constexpr int TBLK = 1024;
 constexpr int TBLK_SMALL = 256;
 constexpr int TBLK_SMALL_NPAD = 32768;
@@ -47,7 +49,8 @@ constexpr int GRAM_WAVES = 8;  // chains per gram workgroup
 constexpr int TM_PW = 16;      // panel width of the timing-model elimination
 
 struct LScratch {
-  double* G;   // [C][mp*mp] Gram / factor (row-major, lower triangle)
+  double* G;   // [C][mp*mp] Gram (row-major, lower triangle); kept for the floor pass
+  double* G2;  // [C][mp*mp] lg_tmelim's output: timing-model factor + Schur complement S0
   double* y;   // [C][npad]  r - T b
   double* w;   // [C][npad]  1/N (white scratch: y^2/a during the white block)
   double* sc;  // [C][16]    per-chain scalars (SC_*)
@@ -62,6 +65,9 @@ enum : int {
   SC_XLAST = 5,
   SC_REDRAW = 6,
   SC_FB = 7,
+  SC_TMPMIN = 8,   // smallest / largest pivot of the real timing-model columns
+  SC_TMPMAX = 9,
+  SC_FLOOR = 10,   // the b draw's SVD noise floor f (floor_shift), 0: the exact draw
 };
 
 struct LArgs {
@@ -76,6 +82,7 @@ struct LArgs {
   long long sweep0, chain0;
   int eval_only;
   double *out_w, *out_h;
+  int floor_pass;  // 1: the b draw's floor pass (lg_tmelim + hyper on chains with SC_FLOOR > 0)
 };
 
 // Dataset of chain c (dataset batches: one DevModel per dataset).  Chains of one 16-chain
@@ -294,7 +301,7 @@ __global__ void __launch_bounds__(TB) lg_white(const DevModel* __restrict__ mds,
       double zv[WU], av[WU], yw[WU];
 #pragma unroll
       for (int k = 0; k < WU; ++k) {
-        const int t = t0 + k * TB < n ? t0 + k * TB : (int)threadIdx.x;
+        const int t = t0 + k * TB < n ? t0 + k * TB : min((int)threadIdx.x, n - 1);  // in-bounds, masked below
         zv[k] = zc[t];
         av[k] = alc[t];
         yw[k] = yc[t];
@@ -330,7 +337,7 @@ __global__ void __launch_bounds__(TB) lg_white(const DevModel* __restrict__ mds,
           double sv[U], wv[U];
 #pragma unroll
           for (int k = 0; k < U; ++k) {
-            const int t = t0 + k * TB < n ? t0 + k * TB : (int)threadIdx.x;
+            const int t = t0 + k * TB < n ? t0 + k * TB : min((int)threadIdx.x, n - 1);  // in-bounds, masked below
             sv[k] = s2[t];
             wv[k] = w2[t];
           }
@@ -389,7 +396,7 @@ __global__ void __launch_bounds__(TB) lg_white(const DevModel* __restrict__ mds,
     int bv[WU];
 #pragma unroll
     for (int k = 0; k < WU; ++k) {
-      const int t = t0 + k * TB < n ? t0 + k * TB : (int)threadIdx.x;
+      const int t = t0 + k * TB < n ? t0 + k * TB : min((int)threadIdx.x, n - 1);  // in-bounds, masked below
       zv[k] = zc[t];
       av[k] = alc[t];
       sv[k] = wf.s2[t];
@@ -672,24 +679,32 @@ __global__ void __launch_bounds__(64 * GS_WPB) lg_gram_small(const DevModel* __r
 __global__ void __launch_bounds__(LBLK) lg_tmelim(const DevModel* __restrict__ mds, LArgs a) {
   const int c = blockIdx.x;
   const DevModel& md = mds[ds_of(a, c)];
+  double* sc = a.s.sc + (size_t)c * 16;
+  // floor pass: only the chains whose b draw runs at the SVD noise floor, with Sigma + f I
+  const double fsh = a.floor_pass ? sc[SC_FLOOR] : 0.0;
+  if (a.floor_pass && !(fsh > 0.0)) return;
   extern __shared__ double lsm[];
   constexpr int PS = TM_PW + 1;        // panel row stride
   double* P = lsm;                     // [mp][PS]
   __shared__ double ainv[TM_PW];
   __shared__ double red[4];
   const int mp = md.mp, K0 = md.ntm_pad, raug = md.raug;
-  double* Gc = a.s.G + (size_t)c * mp * mp;
+  // G stays the Gram (the floor pass re-eliminates it); the factor and S0 go to G2: the
+  // first panel reads G, every later read is of G2
+  const double* Gg = a.s.G + (size_t)c * mp * mp;
+  double* Gc = a.s.G2 + (size_t)c * mp * mp;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  double ld = 0.0, quad = 0.0;
+  double ld = 0.0, quad = 0.0, pmin = INFINITY, pmax = 0.0;
   int fail = 0;
   for (int k0 = 0; k0 < K0; k0 += TM_PW) {
     const int R = mp - k0;
+    const double* Gin = k0 == 0 ? Gg : Gc;
     // load the panel; timing-model prior 1/tm_weight on its diagonal, unit pivots on pads
     for (int e = tid; e < R * TM_PW; e += LBLK) {
       const int i = e / TM_PW, kk = e % TM_PW;
       const int gi = k0 + i, gk = k0 + kk;
-      double v = (gi >= gk) ? Gc[(size_t)gi * mp + gk] : 0.0;
-      if (gi == gk) v = (gk < md.ntm) ? v + md.tm_phiinv : 1.0;
+      double v = (gi >= gk) ? Gin[(size_t)gi * mp + gk] : 0.0;
+      if (gi == gk) v = (gk < md.ntm) ? (v + md.tm_phiinv) + fsh : 1.0;
       P[i * PS + kk] = v;
     }
     __syncthreads();
@@ -704,6 +719,10 @@ __global__ void __launch_bounds__(LBLK) lg_tmelim(const DevModel* __restrict__ m
       }
       if (tid == 0) {
         fail |= !(akk > 0.0) ? 1 : 0;
+        if (k0 + kk < md.ntm) {
+          pmin = fmin(pmin, akk);
+          pmax = fmax(pmax, akk);
+        }
         ld += log(akk);
         const double zr = P[(raug - k0) * PS + kk];
         quad += zr * zr * r;
@@ -727,7 +746,7 @@ __global__ void __launch_bounds__(LBLK) lg_tmelim(const DevModel* __restrict__ m
       const int r0 = k1 + 16 * X, c0 = k1 + 16 * Y;
       v4d acc;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) acc[g] = Gc[(size_t)(r0 + (lane >> 4) + 4 * g) * mp + c0 + (lane & 15)];
+      for (int g = 0; g < 4; ++g) acc[g] = Gin[(size_t)(r0 + (lane >> 4) + 4 * g) * mp + c0 + (lane & 15)];
 #pragma unroll
       for (int k4 = 0; k4 < TM_PW / 4; ++k4) {
         const int kk = 4 * k4 + (lane >> 4);
@@ -741,10 +760,11 @@ __global__ void __launch_bounds__(LBLK) lg_tmelim(const DevModel* __restrict__ m
     __syncthreads();
   }
   if (tid == 0) {
-    double* sc = a.s.sc + (size_t)c * 16;
     sc[SC_LDTM] = ld;
     sc[SC_QUADTM] = quad;
     sc[SC_FAILTM] = (double)fail;
+    sc[SC_TMPMIN] = pmin;
+    sc[SC_TMPMAX] = pmax;
   }
   (void)red;
 }
@@ -775,7 +795,10 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
   __shared__ double bc[4];
   const int tid = threadIdx.x;
   double* sc = a.s.sc + (size_t)c * 16;
-  const double* Gc = a.s.G + (size_t)c * mp * mp;
+  // floor pass: only the chains whose b draw runs at the SVD noise floor (SC_FLOOR > 0)
+  const double fsh = a.floor_pass ? sc[SC_FLOOR] : 0.0;
+  if (a.floor_pass && !(fsh > 0.0)) return;
+  const double* Gc = (K0 > 0 ? a.s.G2 : a.s.G) + (size_t)c * mp * mp;
   const Rng rng = make_rng(a, c);
   const double* tp = tape_row(a, c);
   XVec xv;
@@ -785,22 +808,23 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
   const int fail_tm = sc[SC_FAILTM] != 0.0;
   const double x_last0 = sc[SC_XLAST];
   int status = fail_tm ? 1 : 0;
-  if (!a.eval_only && tid < NHYPER) mh_variate(md, rng, tp, NWHITE + tid, mhv[tid]);
+  if (!a.eval_only && !a.floor_pass && tid < NHYPER) mh_variate(md, rng, tp, NWHITE + tid, mhv[tid]);
 
-  // factor S0 + diag(phi^-1(q)) in LDS; returns the b-marginalised lnL (gibbs.py:288-329)
+  // factor S0 + diag(phi^-1(q)) in LDS (+ f I in the floor pass); returns the b-marginalised
+  // lnL (gibbs.py:288-329)
   auto lnl = [&](const XVec& q, int& failed) -> double {
     const double lA = xget(q, md.idx_logA);
     const double g = xget(q, md.idx_gamma);
     const double lc = 2.0 * lA * 2.302585092994045684 - md.log_12pi2 + (g - 3.0) * md.log_fyr;
     for (int f = tid; f < nf; f += LBLK) {
       if (f < nfr) {
-        ph[f] = exp(-(lc - g * md.lfreq[f] + md.ldf[f]));
+        ph[f] = exp(-(lc - g * md.lfreq[f] + md.ldf[f])) + fsh;
       } else {
         const int b = md.ecb[f - nfr];
         int pi = md.ecorr_b[0];
 #pragma unroll
         for (int j = 1; j < NBMAX; ++j) pi = (b == j) ? md.ecorr_b[j] : pi;
-        ph[f] = exp(-2.0 * xget(q, pi) * 2.302585092994045684);
+        ph[f] = exp(-2.0 * xget(q, pi) * 2.302585092994045684) + fsh;
       }
     }
     double logdet_phi = ((double)nfr * lc - g * md.sum_lfreq + md.sum_ldf) + md.logdet_phi_tm;
@@ -847,7 +871,8 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
   if (run) {
     __syncthreads();
     double l0 = 0.0, p0 = 0.0;
-    const int first = ((a.mask & 2u) || a.eval_only) ? -1 : NHYPER;
+    // the floor pass refactors the final x only (its MH decisions stand)
+    const int first = ((a.mask & 2u) || a.eval_only) && !a.floor_pass ? -1 : NHYPER;
     for (int step = first; step <= NHYPER; ++step) {
       XVec q;
       double luacc = 0.0;
@@ -902,13 +927,35 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
     }
   }
   if (a.eval_only) return;
+  // the SVD noise floor (floor_shift): pivots of the real columns, timing model and hyper block
+  double fs = 0.0;
+  if (!a.floor_pass && redraw && !fb && !(a.st.debug & DEBUG_EXACT_BDRAW)) {
+    double mn = INFINITY, mx = 0.0;
+    for (int k = tid; k < nf; k += LBLK) {
+      mn = fmin(mn, S[k * SS + k]);
+      mx = fmax(mx, S[k * SS + k]);
+    }
+    mx = wave_max(mx);
+    mn = -wave_max(-mn);
+    if ((tid & 63) == 0) {
+      red[tid >> 6] = mx;
+      bc[tid >> 6] = mn;
+    }
+    __syncthreads();
+    mx = fmax(fmax(fmax(red[0], red[1]), fmax(red[2], red[3])), sc[SC_TMPMAX]);
+    mn = fmin(fmin(fmin(bc[0], bc[1]), fmin(bc[2], bc[3])), sc[SC_TMPMIN]);
+    fs = floor_of(mn, mx);
+    __syncthreads();
+  }
   if (tid < md.P) a.st.x[(size_t)c * md.P + tid] = xget(xv, tid);
   if (tid == 0) {
     sc[SC_REDRAW] = redraw ? 1.0 : 0.0;
     sc[SC_FB] = (double)fb;
-    if (a.st.status) a.st.status[c] |= status | ((redraw && fb) ? 2 : 0);
+    if (!a.floor_pass) sc[SC_FLOOR] = fs;
+    if (a.st.status)
+      a.st.status[c] |= status | ((redraw && fb) ? 2 : 0) | (fs > 0.0 ? STATUS_FLOOR : 0);
   }
-  if (!redraw || fb) return;
+  if (!redraw || fb || fs > 0.0) return;   // fs > 0: the floor pass draws b
   // b draw, Fourier block: w_k = zraw_k y_k + eta_k, then L^T v = w (raw columns, pivots on
   // the diagonal, y_k = 1/sqrt(a_kk)); back substitution in axpy form over rows of S
   double* vF = a.s.v + (size_t)c * mp + K0;
@@ -987,7 +1034,10 @@ __global__ void __launch_bounds__(64 * HR_WPB) lg_hyper_reg(const DevModel* __re
   const int p = lane >> 3, q = lane & 7;
   const int nf = md.nf + md.nec, nfr = md.nf, K0 = md.ntm_pad, mp = md.mp;
   double* sc = a.s.sc + (size_t)c * 16;
-  const double* Gc = a.s.G + (size_t)c * mp * mp;
+  // floor pass: only the chains whose b draw runs at the SVD noise floor (SC_FLOOR > 0)
+  const double fsh = a.floor_pass ? sc[SC_FLOOR] : 0.0;
+  if (a.floor_pass && !(fsh > 0.0)) return;
+  const double* Gc = (K0 > 0 ? a.s.G2 : a.s.G) + (size_t)c * mp * mp;
   const Rng rng = make_rng(a, c);
   const double* tp = tape_row(a, c);
   XVec xv;
@@ -997,7 +1047,8 @@ __global__ void __launch_bounds__(64 * HR_WPB) lg_hyper_reg(const DevModel* __re
   const int fail_tm = sc[SC_FAILTM] != 0.0;
   const double x_last0 = sc[SC_XLAST];
   int status = fail_tm ? 1 : 0;
-  if (!a.eval_only && lane < NHYPER) mh_variate(md, rng, tp, NWHITE + lane, mhv + 4 * lane);
+  if (!a.eval_only && !a.floor_pass && lane < NHYPER)
+    mh_variate(md, rng, tp, NWHITE + lane, mhv + 4 * lane);
   // S0 from the Gram's trailing block (lg_tmelim left the Schur complement there), in the
   // cyclic layout: slot (r, s), lane (p, q) = internal (8r+p, 8s+q); diagonal slots hold the
   // full symmetric 8x8 block
@@ -1022,13 +1073,13 @@ __global__ void __launch_bounds__(64 * HR_WPB) lg_hyper_reg(const DevModel* __re
     const double lc = 2.0 * lA * 2.302585092994045684 - md.log_12pi2 + (g - 3.0) * md.log_fyr;
     double pv = 0.0;                    // phi^-1 of internal column `lane` (0: none)
     if (lane < nfr) {
-      pv = exp(-(lc - g * md.lfreq[lane] + md.ldf[lane]));
+      pv = exp(-(lc - g * md.lfreq[lane] + md.ldf[lane])) + fsh;
     } else if (lane < nf) {
       const int b = md.ecb[lane - nfr];
       int pi = md.ecorr_b[0];
 #pragma unroll
       for (int j = 1; j < NBMAX; ++j) pi = (b == j) ? md.ecorr_b[j] : pi;
-      pv = exp(-2.0 * xget(xq, pi) * 2.302585092994045684);
+      pv = exp(-2.0 * xget(xq, pi) * 2.302585092994045684) + fsh;
     }
     ph[lane] = pv;
     double logdet_phi = ((double)nfr * lc - g * md.sum_lfreq + md.sum_ldf) + md.logdet_phi_tm;
@@ -1064,7 +1115,8 @@ __global__ void __launch_bounds__(64 * HR_WPB) lg_hyper_reg(const DevModel* __re
   lds_order();
   if (run) {
     double l0 = 0.0, p0 = 0.0;
-    const int first = ((a.mask & 2u) || a.eval_only) ? -1 : NHYPER;
+    // the floor pass refactors the final x only (its MH decisions stand)
+    const int first = ((a.mask & 2u) || a.eval_only) && !a.floor_pass ? -1 : NHYPER;
     for (int step = first; step <= NHYPER; ++step) {
       XVec xq;
       double luacc = 0.0;
@@ -1118,13 +1170,23 @@ __global__ void __launch_bounds__(64 * HR_WPB) lg_hyper_reg(const DevModel* __re
     }
   }
   if (a.eval_only) return;
+  // the SVD noise floor (floor_shift): pivots of the real columns, timing model and hyper block
+  double fs = 0.0;
+  if (!a.floor_pass && redraw && !fb && !(a.st.debug & DEBUG_EXACT_BDRAW)) {
+    double mn, mx;
+    const double ap[2] = {apr[0], 1.0};
+    pivot_range(ap, lane, 0, 0, nf, mn, mx);
+    fs = floor_of(fmin(mn, sc[SC_TMPMIN]), fmax(mx, sc[SC_TMPMAX]));
+  }
   if (lane < md.P) a.st.x[(size_t)c * md.P + lane] = xget(xv, lane);
   if (lane == 0) {
     sc[SC_REDRAW] = redraw ? 1.0 : 0.0;
     sc[SC_FB] = (double)fb;
-    if (a.st.status) a.st.status[c] |= status | ((redraw && fb) ? 2 : 0);
+    if (!a.floor_pass) sc[SC_FLOOR] = fs;
+    if (a.st.status)
+      a.st.status[c] |= status | ((redraw && fb) ? 2 : 0) | (fs > 0.0 ? STATUS_FLOOR : 0);
   }
-  if (!redraw || fb) return;
+  if (!redraw || fb || fs > 0.0) return;   // fs > 0: the floor pass draws b
   // b draw, hyper block (lg_hyper's back substitution): the raw factor goes to the S0 region
   // ([slot][lane]: a_ik at 64 SL(i/8, k/8) + 8 (i%8) + k%8); lane k owns column k
 #pragma unroll
@@ -1178,7 +1240,7 @@ __global__ void __launch_bounds__(LBLK) lg_btm(const DevModel* __restrict__ mds,
   const int tid = threadIdx.x;
   const double* sc = a.s.sc + (size_t)c * 16;
   if (sc[SC_REDRAW] == 0.0 || sc[SC_FB] != 0.0) return;
-  const double* Gc = a.s.G + (size_t)c * mp * mp;
+  const double* Gc = a.s.G2 + (size_t)c * mp * mp;   // lg_tmelim's factor (K0 > 0 here)
   double* v = a.s.v + (size_t)c * mp;
   const Rng rng = make_rng(a, c);
   const double* tp = tape_row(a, c);

@@ -125,10 +125,11 @@ def _grid_on_device(thetas, realisations, models, seed, sigma_out, red_source, d
 # A record is "in the all-outlier state" when at least half of its TOAs are flagged
 # (sum z >= n / 2).  vvh17 chains start there (z = 1 with alpha fixed at 1e10, gibbs.py:44-51:
 # every TOA is effectively removed, b is drawn from its prior, q ~ 1 keeps z = 1).  The
-# reference's chains leave within ~100-200 sweeps only through the error of its SVD draw at
-# cond(Sigma) ~ 1e22 (gibbs.py:169-180); with the exact Cholesky draw a chain can stay for
-# thousands of sweeps (tools/vvh17_protocol.py), so the study reports
-# the fraction of such records per entry and warns when a vvh17 entry keeps any.
+# reference's chains leave within ~100 sweeps through its SVD draw's rounding floor at
+# cond(Sigma) ~ 1e22 (gibbs.py:169-180), which the HIP path reproduces (include/gst.h
+# gst_sweep; with the exact draw a chain stays for thousands of sweeps).
+# The study still reports the fraction of such records per entry and warns when a vvh17
+# entry keeps any.
 TRAP_WARN_FRAC = 0.01
 
 
@@ -136,9 +137,8 @@ def initial_state(entry: Entry, chains: int, gid0: int, seed: int, nst: int,
                   vvh17_start: str = "reference"):
     """Prior draw per chain (run_sims.py:111) and the gibbs.py:29-51 latent initial state.
 
-    ``vvh17_start="clean"`` starts vvh17 chains with no TOA flagged (z = 0) instead of the
-    reference's all-outlier start (z = 1, gibbs.py:50-51), which the exact b draw leaves
-    only slowly (see TRAP_WARN_FRAC above)."""
+    ``vvh17_start="clean"`` (opt-in) starts vvh17 chains with no TOA flagged (z = 0) instead
+    of the reference's all-outlier start (z = 1, gibbs.py:50-51)."""
     if vvh17_start not in ("reference", "clean"):
         raise ValueError("vvh17_start must be 'reference' or 'clean'")
     pta, cfg = entry.pta, entry.cfg
@@ -163,11 +163,11 @@ def initial_state(entry: Entry, chains: int, gid0: int, seed: int, nst: int,
 class Study:
     """A batch of entries x ``chains`` chains on one GPU (one NativeSampler).
 
-    ``vvh17_start``: "clean" (default) starts vvh17 chains with no TOA flagged; "reference"
-    with gibbs.py's z = 1, which the exact b draw leaves slowly (TRAP_WARN_FRAC above)."""
+    ``vvh17_start``: "reference" (default) starts vvh17 chains as gibbs.py:50-51 does (z = 1);
+    "clean" (opt-in) with no TOA flagged."""
 
     def __init__(self, entries, chains=1, device=0, seed=1, entry0=0,
-                 vvh17_start="clean"):
+                 vvh17_start="reference"):
         from .native import NativeSampler
         self.entries = list(entries)
         self.chains = int(chains)
@@ -183,6 +183,7 @@ class Study:
                  for i, e in enumerate(self.entries)]
         self.ns.set_state(**{k: np.concatenate([p[k] for p in parts]) for k in parts[0]})
         self.sweeps_done = 0
+        self.vvh17_start = vvh17_start
         self.trapped = None
 
     @property
@@ -266,11 +267,12 @@ class Study:
             row = {"entry": self.entry0 + i, "kind": e.kind, "theta": e.theta, "idx": e.idx,
                    "model": e.model, "source": src, "trapped_record_frac": frac,
                    "trapped_chain_frac_end": end}
+            if e.model == "vvh17":
+                row["vvh17_start"] = self.vvh17_start
             if e.model == "vvh17" and frac > TRAP_WARN_FRAC:
                 row["warning"] = (
-                    f"{frac:.1%} of the kept records sit in the all-outlier start state "
-                    "(sum z >= n/2): the exact b draw leaves gibbs.py's z = 1 start slowly; "
-                    "burn in longer or use vvh17_start='clean' (DESIGN.md section 3)")
+                    f"{frac:.1%} of the kept records sit in the all-outlier state (sum z >= "
+                    f"n/2; start '{self.vvh17_start}'): burn in longer (DESIGN.md section 3)")
                 import sys
                 print(f"run_sims WARNING entry {self.entry0 + i} ({e.kind}, theta={e.theta}, "
                       f"vvh17): {row['warning']}", file=sys.stderr, flush=True)
@@ -368,11 +370,9 @@ def main(argv=None):
                     help="draw the grid's datasets in one GPU launch (default) or per "
                          "dataset with NumPy")
     ap.add_argument("--red-source", choices=("powerlaw", "red.txt"), default="powerlaw")
-    ap.add_argument("--vvh17-start", choices=("reference", "clean"), default="clean",
-                    help="vvh17 initial outlier flags: z = 0 (default: at the reference's "
-                         "10000-sweep protocol its [100:] records match the reference's "
-                         "posterior, KS p >= 0.68) or the reference's z = 1 (gibbs.py:50-51), "
-                         "which the exact b draw leaves only after ~1000-5000 sweeps")
+    ap.add_argument("--vvh17-start", choices=("reference", "clean"), default="reference",
+                    help="vvh17 initial outlier flags: the reference's z = 1 (gibbs.py:50-51, "
+                         "default) or z = 0")
     args = ap.parse_args(argv)
     from . import dist
     rank, local, world = dist.init()
@@ -391,7 +391,7 @@ def main(argv=None):
                         record_every=args.record_every)
     total = len(mine) * args.chains * args.niter
     print(json.dumps({"rank": rank, "entries": len(mine), "chains": args.chains,
-                      "sweeps": args.niter, "seconds": secs,
+                      "sweeps": args.niter, "vvh17_start": args.vvh17_start, "seconds": secs,
                       "chain_sweeps_per_s": total / secs}), flush=True)
     for row in st.trapped or []:
         if row["trapped_record_frac"] > 0:

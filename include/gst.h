@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GST_ABI_VERSION 3
+#define GST_ABI_VERSION 4
 
 /* Outlier model kind: Gibbs(model=...) (gibbs.py:9,32,187-226). */
 enum gst_outlier_model {
@@ -116,7 +116,9 @@ typedef struct gst_model_desc {
  *   status & 2 (bit 1)  the b-draw factorisation failed and b was kept;
  *   status & 4 (bit 2)  dataset index out of range: the persistent path does not run the
  *                       chain, the large path runs it on dataset 0;
- *   status & 8 (bit 3)  large path: the chain's aligned 16-chain group mixes datasets.
+ *   status & 8 (bit 3)  large path: the chain's aligned 16-chain group mixes datasets;
+ *   status & 16 (bit 4) informational: a b draw ran at the SVD noise floor (Sigma beyond
+ *                       fp64 resolution, e.g. vvh17's all-outlier start; see gst_sweep).
  * dataset[C] gives each chain's dataset index into the batch passed to
  * gst_model_set_batch; it may be NULL when there is one dataset. */
 typedef struct gst_state {
@@ -184,7 +186,14 @@ int gst_model_info(void* ctx, int* ndatasets, int* nmax, int* tape_stride);
 /* Run `nsweeps` Gibbs sweeps for chains [0, nchains) (Gibbs.sample's loop body,
  * gibbs.py:354-380).  `tape` NULL or tape->data NULL -> on-device Philox4x32-10 variates
  * keyed by (seed, chain0 + c), counters by (sweep0 + i, stage, index): results do not
- * depend on how chains are sharded over launches or GPUs. */
+ * depend on how chains are sharded over launches or GPUs.
+ * b draw (gibbs.py:145-182): exact Cholesky draw b = Sigma^-1 d + L^-T eta, except where
+ * Sigma is beyond fp64 resolution -- its smallest LDL^T pivot (timing-model-first order, real
+ * columns) below 1e-14 of its largest, p_max.  There the reference's sl.svd returns the small
+ * eigenvalues at LAPACK's rounding floor (~eps x s_max) and its draw is that of Sigma + f I;
+ * this path draws from Sigma + f I with f = 0.5 x 2^-52 p_max (and flags status & 16), which
+ * reproduces the reference's escape from vvh17's all-outlier start.
+ * GST_DEBUG_EXACT_BDRAW turns the floor off. */
 int gst_sweep(void* ctx, const gst_state* state, const gst_records* rec,
               const gst_tape* tape, int nchains, int nsweeps, long long sweep0,
               int record_every, unsigned stage_mask, unsigned long long seed,
@@ -231,7 +240,14 @@ int gst_set_waves(void* ctx, int waves);
  * GST_DEBUG_LARGE_HYPER forces the LDS-resident hyper kernel (lg_hyper) where the register-
  * resident one (lg_hyper_reg) would run: same variates and decisions, likelihoods within
  * rounding.  Test switches (the defaults are the faster kernels). */
-enum gst_debug { GST_DEBUG_POISON = 1, GST_DEBUG_LARGE_GRAM = 2, GST_DEBUG_LARGE_HYPER = 4 };
+/* GST_DEBUG_EXACT_BDRAW: every b draw is the exact draw from Sigma, also beyond fp64
+ * resolution (no SVD noise floor, see gst_sweep). */
+enum gst_debug {
+  GST_DEBUG_POISON = 1,
+  GST_DEBUG_LARGE_GRAM = 2,
+  GST_DEBUG_LARGE_HYPER = 4,
+  GST_DEBUG_EXACT_BDRAW = 8
+};
 int gst_set_debug(void* ctx, int flags);
 
 /* Per-kernel timing of the large path (HIP events around every launch of the next

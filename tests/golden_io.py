@@ -63,12 +63,13 @@ def sweep_tape(ref, i):
     return {k: v[i] for k, v in ref["tape"].items()}
 
 
-def oracle_chol_replay(ref, S=None):
+def oracle_replay(ref, S=None):
     """The oracle replaying the reference's tape for S sweeps from the recorded start with
     the Cholesky mean and the recorded draw term (b = cho_solve(Sigma, d) + b_delta,
-    gibbs.py:321-322 + 169-180).  That is the expression the HIP path evaluates in tape
-    mode, so the two chains agree to fp64 rounding, not to the SVD-vs-Cholesky mean gap
-    that separates both from the reference's own chain.  Returns records {key: [S, ...]}
+    gibbs.py:321-322 + 169-180; at the SVD noise floor, Sigma beyond fp64 resolution, the
+    mean of Sigma + f I: Oracle.floor_shift).  That is the expression the HIP path evaluates
+    in tape mode, so the two chains agree to fp64 rounding, not to the SVD-vs-Cholesky mean
+    gap that separates both from the reference's own chain.  Returns records {key: [S, ...]}
     of the state at the start of each sweep (gibbs.py:355-361)."""
     import warnings
 
@@ -87,5 +88,5 @@ def oracle_chol_replay(ref, S=None):
                          ("alpha", st.alpha), ("pout", st.pout), ("theta", st.theta),
                          ("nu", float(st.nu))):
                 rec[k].append(np.array(v, dtype=np.float64, copy=True))
-            x = orc.sweep(st, x, TapeVariates(sweep_tape(ref, i)), b_mean="chol_delta")
+            x = orc.sweep(st, x, TapeVariates(sweep_tape(ref, i)), b_mean="floor_delta")
     return {k: np.stack(v) for k, v in rec.items()}

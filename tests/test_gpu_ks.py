@@ -10,6 +10,7 @@ sweeps; the test keeps every second of those draws on both sides, i.e. 50 sweeps
 beyond the integrated autocorrelation time of every marginal (about 40 sweeps for gamma,
 bench.py ESS), so the draws are close to independent as the KS test assumes).
 """
+import json
 import os
 
 import numpy as np
@@ -24,29 +25,27 @@ torch = pytest.importorskip("torch")
 if not torch.cuda.is_available():  # pragma: no cover
     pytest.skip("needs a HIP device", allow_module_level=True)
 
+from gibbs_student_t_amd._abi import STATUS_FLOOR  # noqa: E402
 from gibbs_student_t_amd.native import NativeSampler  # noqa: E402
 from gibbs_student_t_amd.run_sims import MODELS, TRAP_WARN_FRAC  # noqa: E402
 
 P_MIN = 1e-3
 # vvh17 starts every chain with all TOAs flagged as outliers (z = 1, gibbs.py:50-51) and a
-# fixed alpha = 1e10, so at first every TOA is effectively removed from the fit, b is drawn
-# from its prior, and q ~ 1 keeps z = 1: a metastable all-outlier state that an exact b draw
-# leaves only slowly.  The reference's chains leave it within ~200 sweeps only through its SVD
-# square root of a Sigma with cond ~ 1e22 (tests/golden/ref_vvh17_*.npz): the oracle with the
-# reference's SVD draw escapes in 100-200 sweeps, the same oracle with only the b draw made
-# exact (Cholesky) stays trapped for 900-1500+ (tools/diag/vvh17_trap_cpu.py).  Measured on
-# the GPU at the reference's study protocol (tools/vvh17_protocol.py, profiles/
-# r3_vvh17_protocol.json): 100% of 1024 chains trapped at sweep 500, 78% at 1000, 25% at
-# 2000, 1.5% at 5000, 0.3% at 10000.  So this comparison burns in longer, and drops the
-# chains whose window still sits in that state by the documented criterion
-# (run_sims.TRAP_WARN_FRAC: sum z >= n/2, i.e. theta >= 1/2 for vvh17's uniform theta
-# prior, theta ~ Beta(sum z + 1, n - sum z + 1)), applied to BOTH samples' chains.
-VVH17_BURN = 30000
+# fixed alpha = 1e10, so at first every TOA is effectively removed from the fit and Sigma's
+# condition number is ~1e22.  The reference's SVD b draw (gibbs.py:169-180) returns the
+# smallest eigenvalues at LAPACK's rounding floor, which narrows the timing-model part of the
+# draw; that is how its chains leave this all-outlier state within ~100 sweeps (the exact
+# draw stays in it for thousands).  The HIP path reproduces the floor (include/gst.h
+# gst_sweep: the exact draw from Sigma + f I there, status & 16), so the reference's start
+# and burn-in are used unchanged; tests/golden/vvh17_escape_ref.json holds the escape
+# sweeps of the reference algorithm itself (the oracle with gibbs.py's legacy RNG and SVD
+# draw, tools/vvh17_escape.py) from 256 prior draws.
+TRAPPED = 0.5      # all-outlier state: sum z >= n / 2 (run_sims.TRAP_WARN_FRAC's criterion)
 
 
 def _all_outlier_chains(theta):
     """Chains whose window-mean theta is >= 1/2: the all-outlier state (see above)."""
-    return theta.mean(axis=1) >= 0.5
+    return theta.mean(axis=1) >= TRAPPED
 
 
 @pytest.mark.parametrize("model", ["beta", "t", "gaussian", "uniform", "vvh17"])
@@ -56,8 +55,6 @@ def test_posterior_marginals_match_reference(model):
     burn, thin = int(ref["burn"]), 2 * int(ref["thin"])
     rx, rth, rnu = ref["x"][:, ::2], ref["theta"][:, ::2], ref["nu"][:, ::2]
     pta = load_dataset()
-    if model == "vvh17":
-        burn = VVH17_BURN
     C, S = 1024, burn + 60 * thin
     ns = NativeSampler(pta, MODELS[model], 0)
     ns.alloc(C)
@@ -72,17 +69,12 @@ def test_posterior_marginals_match_reference(model):
     rec = ns.alloc_records(S - burn, keys=("x", "theta", "nu"))
     ns.sweep(S - burn, records=rec, seed=77, sweep0=burn)
     got = {k: v.cpu().numpy()[:, ::thin] for k, v in rec.items()}
-    assert np.all(ns.get_state()["status"] == 0)
+    assert np.all((ns.get_state()["status"] & ~STATUS_FLOOR) == 0)
     if model == "vvh17":
-        # the same documented criterion on both samples: chains still in the all-outlier
-        # state are unconverged, not samples of the posterior; they must be rare here, and
-        # the reference's chains (burn-in 1000, escaped through the SVD draw) have none
-        trapped = _all_outlier_chains(got["theta"])
-        assert trapped.mean() <= 0.01, f"{trapped.sum()} vvh17 chains in the all-outlier state"
-        got = {k: v[~trapped] for k, v in got.items()}
-        rtrap = _all_outlier_chains(rth)
-        assert not rtrap.any()
-        rx, rth, rnu = rx[~rtrap], rth[~rtrap], rnu[~rtrap]
+        # the reference's own start and burn-in (1000): no chain of either sampler is left in
+        # the all-outlier state, and none is dropped
+        assert not _all_outlier_chains(got["theta"]).any()
+        assert not _all_outlier_chains(rth).any()
     names = [str(s) for s in ref["names"]]
     series = [(nm, got["x"][..., j].ravel(), rx[..., j].ravel())
               for j, nm in enumerate(names)]
@@ -97,39 +89,79 @@ def test_posterior_marginals_match_reference(model):
     ns.close()
 
 
-def _vvh17_protocol_run(start, C=1024, seed=31):
+def _vvh17_protocol_run(start, C=1024, seed=31, exact=False, sweeps=10000, chunk=100):
     """vvh17 at the reference study's protocol: 10000 sweeps from prior draws, records
     [100:] (run_sims.py:110-124), from the reference's z = 1 start or run_sims' 'clean'
-    z = 0 start; returns the window draws and the all-outlier fraction every 100 sweeps."""
+    z = 0 start; returns the window draws, the all-outlier fraction every `chunk` sweeps and
+    each chain's escape sweep (end of the first chunk with sum z < n / 2; -1: never).
+    ``exact``: GST_DEBUG_EXACT_BDRAW (no SVD noise floor)."""
     pta = load_dataset()
     n = pta.n
     ns = NativeSampler(pta, MODELS["vvh17"], 0)
     ns.alloc(C)
+    ns.set_debug(exact_bdraw=exact)
     lo = np.array([p.pmin for p in pta.params])
     hi = np.array([p.pmax for p in pta.params])
     x0 = np.stack([np.random.default_rng([seed, c]).uniform(lo, hi) for c in range(C)])
     ns.set_state(x=x0, z=np.full((C, n), 1.0 if start == "reference" else 0.0),
                  alpha=np.full((C, n), 1e10), theta=np.full(C, 0.01), nu=np.full(C, 4.0))
     xs, th, frac = [], [], []
-    for k in range(100):
-        rec = ns.alloc_records(100, keys=("x", "theta"))
-        ns.sweep(100, records=rec, seed=seed, sweep0=100 * k)
-        z = ns.state["z"][:, :n].sum(1)
-        frac.append(float((z >= 0.5 * n).double().mean()))
+    esc = np.full(C, -1)
+    for k in range(sweeps // chunk):
+        rec = ns.alloc_records(chunk, keys=("x", "theta"))
+        ns.sweep(chunk, records=rec, seed=seed, sweep0=chunk * k)
+        z = ns.state["z"][:, :n].sum(1).cpu().numpy()
+        frac.append(float(np.mean(z >= TRAPPED * n)))
+        esc[(esc < 0) & (z < TRAPPED * n)] = chunk * (k + 1)
         xs.append(rec["x"].cpu().numpy())
         th.append(rec["theta"].cpu().numpy())
-    assert np.all(ns.get_state()["status"] == 0)
+    status = ns.get_state()["status"]
+    assert np.all((status & ~STATUS_FLOOR) == 0)
     ns.close()
-    return np.concatenate(xs, 1)[:, 100:], np.concatenate(th, 1)[:, 100:], frac
+    return np.concatenate(xs, 1)[:, 100:], np.concatenate(th, 1)[:, 100:], frac, esc, status
 
 
-def test_vvh17_reference_protocol_clean_start_matches_reference():
-    """run_sims' default vvh17 start (z = 0) at the reference's own protocol: no chain ever
-    in the all-outlier state and the [100:] window's marginals pass KS against the
+def test_vvh17_reference_start_escapes_as_the_reference():
+    """The reference's own z = 1 start: the chains leave the all-outlier state as the
+    reference algorithm's do (escape sweeps vs the oracle with gibbs.py's SVD draw, binned to
+    the 10-sweep resolution of the run: KS p > 1e-3; trapped fraction at sweep 500 <= 1%, the
+    reference's being 0 of 256), every chain drew at the SVD noise floor at its start, and
+    none is in the all-outlier state at sweep 1000."""
+    with open(os.path.join(GOLDEN, "vvh17_escape_ref.json")) as f:
+        ref = json.load(f)
+    ref_esc = np.array([e if e is not None else 10 ** 6 for e in ref["escape"]], float)
+    _, _, frac, esc, status = _vvh17_protocol_run("reference", sweeps=1000, chunk=10)
+    assert np.all(status & STATUS_FLOOR)
+    assert frac[49] <= 0.01, f"trapped at sweep 500: {frac[49]:.3f}"
+    assert frac[-1] == 0.0 and np.all(esc > 0)
+    p = scipy.stats.ks_2samp(esc, 10 * np.ceil(ref_esc / 10)).pvalue
+    assert p > P_MIN, f"escape sweeps: KS p={p:.2e} (gpu median {np.median(esc)}, " \
+                      f"reference median {np.median(ref_esc)})"
+
+
+def test_vvh17_reference_protocol_reference_start_matches_reference():
+    """run_sims' default vvh17 start -- the reference's z = 1 -- at the reference's own
+    protocol (10000 sweeps, records [100:]): the window's marginals pass KS against the
     reference's posterior draws WITHOUT dropping any chain."""
     ref = np.load(os.path.join(GOLDEN, "posterior_ref_j1713_vvh17.npz"), allow_pickle=False)
     thin = 2 * int(ref["thin"])
-    x, th, frac = _vvh17_protocol_run("clean")
+    x, th, frac, _, _ = _vvh17_protocol_run("reference")
+    assert max(frac[5:]) == 0.0           # nothing left in the all-outlier state after 600
+    names = [str(s) for s in ref["names"]]
+    for j, nm in enumerate(names):
+        p = scipy.stats.ks_2samp(x[:, ::thin, j].ravel(), ref["x"][:, ::2, j].ravel()).pvalue
+        assert p > P_MIN, f"vvh17 reference start {nm}: KS p={p:.2e}"
+    p = scipy.stats.ks_2samp(th[:, ::thin].ravel(), ref["theta"][:, ::2].ravel()).pvalue
+    assert p > P_MIN, f"vvh17 reference start theta: KS p={p:.2e}"
+
+
+def test_vvh17_reference_protocol_clean_start_matches_reference():
+    """run_sims' optional clean vvh17 start (z = 0) at the reference's own protocol: no chain
+    ever in the all-outlier state and the [100:] window's marginals pass KS against the
+    reference's posterior draws WITHOUT dropping any chain."""
+    ref = np.load(os.path.join(GOLDEN, "posterior_ref_j1713_vvh17.npz"), allow_pickle=False)
+    thin = 2 * int(ref["thin"])
+    x, th, frac, _, _ = _vvh17_protocol_run("clean")
     assert max(frac) == 0.0
     names = [str(s) for s in ref["names"]]
     for j, nm in enumerate(names):
@@ -139,12 +171,13 @@ def test_vvh17_reference_protocol_clean_start_matches_reference():
     assert p > P_MIN, f"vvh17 clean start theta: KS p={p:.2e}"
 
 
-def test_vvh17_reference_start_trap_is_the_documented_one():
-    """The reference's z = 1 start with the exact b draw, at the reference's protocol: the
-    all-outlier fraction follows the measured envelope documented in DESIGN.md section 3
-    (every chain trapped through sweep 200, most through 500, nearly none by 10000) --
-    a known behavioural difference from gibbs.py's SVD draw, flagged by run_sims."""
-    _, th, frac = _vvh17_protocol_run("reference")
+def test_vvh17_exact_draw_trap_is_the_documented_one():
+    """The reference's z = 1 start with the EXACT b draw (GST_DEBUG_EXACT_BDRAW: no SVD noise
+    floor), at the reference's protocol: the all-outlier fraction follows the envelope
+    measured in round 3 (every chain trapped through sweep 200, most through 500, nearly
+    none by 10000) -- the behaviour the floor removes."""
+    _, th, frac, _, status = _vvh17_protocol_run("reference", exact=True)
+    assert not np.any(status & STATUS_FLOOR)
     assert frac[1] >= 0.95           # sweep 200
     assert frac[4] >= 0.5            # sweep 500
     assert frac[-1] <= 0.02          # sweep 10000

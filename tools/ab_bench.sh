@@ -9,7 +9,7 @@ for lib in "$@"; do
   [ -n "$AB_QUICK" ] && CFGS=("--steps 500 --warmup 50" "--steps 20 --warmup 5")
   for a in "${CFGS[@]}"; do
     tag=$(echo "$a" | tr -d ' -')
-    GST_LIB=$lib timeout -k 10 120 python -u bench.py --no-cpu-baseline --ess-window 0 $a \
+    GST_ALLOW_ABI_MISMATCH=1 GST_LIB=$lib timeout -k 10 120 python -u bench.py --no-cpu-baseline --ess-window 0 $a \
       > gpurun_out/ab/$n.$tag.json 2> gpurun_out/ab/$n.$tag.err || { echo "FAIL $n $a"; tail -3 gpurun_out/ab/$n.$tag.err; exit 1; }
     python -c "import json,sys;d=json.load(open('gpurun_out/ab/$n.$tag.json'));print('%-14s %-40s %10.0f  kernel %.3f ms/sweep  frac %.3f'%('$n','$a',d['value'],d['kernel_ms']/d['steps'],d['roofline']['frac']))"
   done

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Shared helper for round-3 GPU scripts: run one GPU step under its own time limit; a test
+# Shared helper for GPU job scripts: run one GPU step under its own time limit; a test
 # failure (pytest rc 1) lets the script go on, anything else (timeout, abort, fault) ends it.
 step() {
   local secs=$1 log=$2

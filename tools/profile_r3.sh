@@ -2,7 +2,7 @@
 # Round-3 profile of the current build:   gpurun -- 'bash tools/profile_r3.sh'
 # bench lines (driver command, default, configs 3/4/5), rocprofv3 kernel stats of the
 # 500-sweep headline run, PMC passes of config 2 and of config 5 (one counter group per run).
-source tools/r3/run_guarded.sh
+source tools/gpu_step.sh
 O=gpurun_out/prof_r3; mkdir -p $O
 step 300 $O/bench_driver.json python bench.py --steps 20 --warmup 5
 B="python bench.py --no-cpu-baseline"

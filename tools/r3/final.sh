@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 3 final: full GPU suite, smoke, then the profile run (bench lines, rocprof, PMC)
-source tools/r3/run_guarded.sh
+source tools/gpu_step.sh
 O=gpurun_out/r3final; mkdir -p $O
 step 900 $O/gpu_tests.txt $PYT -m gpu tests/
 grep -h -E "passed|failed" $O/gpu_tests.txt

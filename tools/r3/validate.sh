@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 3 re-entry check of the current build: full GPU suite, smoke, the driver's bench command
-source tools/r3/run_guarded.sh
+source tools/gpu_step.sh
 O=gpurun_out/r3v; mkdir -p $O
 step 900 $O/gpu_tests.txt $PYT -m gpu tests/
 grep -h -E "passed|failed" $O/gpu_tests.txt
