@@ -74,3 +74,40 @@ def test_register_hyper_matches_lds_hyper(pta):
     for k in ("b", "alpha", "pout", "theta"):
         d = np.abs(a[k] - b[k])
         assert np.all(d <= 1e-8 * np.maximum(np.abs(b[k]), 1e-300) + 1e-300), (k, d.max())
+
+
+@pytest.mark.parametrize("name", ["ecb_beta_fixed", "ecb_uniform_fixed", "ecn_t_fixed",
+                                  "ecn_vvh17_fixed"])
+def test_register_hyper_matches_lds_hyper_ecorr(name):
+    """lg_hyper_reg's ECORR and per-backend branches (phi^-1 of the ECORR columns from their
+    backend's log10_ecorr, the ECORR log|phi| term, the b draw over ECORR columns) against
+    lg_hyper on reference fixtures with 44 hyper columns (20 Fourier + 24 ECORR epochs);
+    their parity with the reference itself is test_gpu_parity.py's large-path replays."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    from golden_io import load_ref, sweep_state
+    ref = load_ref(name)
+    s0 = sweep_state(ref, 0)
+    outs = []
+    for large_hyper in (False, True):
+        ns = NativeSampler(ref["pta"], ref["kw"], 0, path="large")
+        ns.set_debug(large_hyper=large_hyper)
+        ns.alloc(C)
+        ns.set_state(x=np.tile(ref["xs"], (C, 1)), b=np.tile(s0["b"], (C, 1)),
+                     z=np.tile(s0["z"], (C, 1)), alpha=np.tile(s0["alpha"], (C, 1)),
+                     pout=np.tile(s0["pout"], (C, 1)), theta=np.full(C, s0["theta"]),
+                     nu=np.full(C, s0["nu"]))
+        rec = ns.alloc_records(S)
+        ns.sweep(S, records=rec, seed=33)
+        out = {k: v.cpu().numpy() for k, v in rec.items()}
+        out["status"] = ns.get_state()["status"]
+        ns.close()
+        outs.append(out)
+    a, b = outs
+    assert np.all((a["status"] & ~STATUS_FLOOR) == 0)
+    np.testing.assert_array_equal(a["status"], b["status"])
+    for k in ("x", "z", "nu"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    for k in ("b", "alpha", "pout", "theta"):
+        d = np.abs(a[k] - b[k])
+        assert np.all(d <= 1e-8 * np.maximum(np.abs(b[k]), 1e-300) + 1e-300), (k, d.max())

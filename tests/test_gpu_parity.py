@@ -33,8 +33,11 @@ PATHS = ("persistent", "large")
 
 
 def _native(ref, C, path="auto"):
-    if path == "persistent" and ref["pta"].T.shape[1] + 1 > 80:
-        pytest.skip("beyond the persistent kernel's shapes (large path only)")
+    pta = ref["pta"]
+    if path == "persistent" and (pta.T.shape[1] + 1 > 80 or pta.n_ecorr > 0
+                                 or len(pta.backend_names) > 1):
+        pytest.skip("beyond the persistent kernel's shapes / white-noise models (large path "
+                    "only)")
     ns = NativeSampler(ref["pta"], ref["kw"], 0, path=path)
     assert path == "auto" or ns.path == path
     ns.alloc(C)

@@ -1,6 +1,6 @@
 """Per-dataset convergence of BASELINE config 4.
 
-    python tools/config4_rhat.py [out.json] [worst.npz]
+    python tools/config4_rhat.py [out.json] [worst.npz] [--save D1,D2,...] [--exact]
 
 Runs bench.py's config-4 workload (256 run_sims datasets x 64 chains on one GPU) with the
 bench's own schedule (300 warmup sweeps, 1000 timed, 3000 burn-in, then a 5000-sweep window
@@ -8,7 +8,11 @@ recorded every 5th sweep), computes rank-normalised split-R-hat and bulk-ESS PER
 for every sampled parameter and theta, and writes every dataset's row (model, kind,
 theta_sim, dof, n, R-hats) sorted by the worst R-hat.  The window draws of the worst
 mixture-model ('beta' / 'uniform') dataset are saved so that tools/config4_oracle.py can
-compare them with the reference algorithm (the oracle) run on the same dataset.
+compare them with the reference algorithm (the oracle) run on the same dataset; ``--save``
+also saves the listed datasets' window draws (<worst stem>_d<D>.npz) for
+tools/config4_same_start.py.  The chains start as bench.workload starts them (prior draws,
+gibbs.py:29-51 latents, vvh17 at the reference's z = 1).  ``--exact``: no SVD noise floor
+in the b draw (GST_DEBUG_EXACT_BDRAW).
 """
 import json
 import os
@@ -27,13 +31,20 @@ W, K, BURN, WIN, THIN, SEED = 300, 1000, 3000, 5000, 5, 20171713
 
 
 def main():
-    dst = sys.argv[1] if len(sys.argv) > 1 else "config4_rhat.json"
-    worst_npz = sys.argv[2] if len(sys.argv) > 2 else None
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    save = []
+    for i, a in enumerate(sys.argv):
+        if a == "--save":
+            save = [int(v) for v in sys.argv[i + 1].split(",")]
+            args.remove(sys.argv[i + 1])
+    dst = args[0] if len(args) > 0 else "config4_rhat.json"
+    worst_npz = args[1] if len(args) > 1 else None
     wl = bench.workload(4, 0, 1, None)
     grid = run_sims.build_grid(thetas=(0.05, 0.1, 0.15), realisations=5,
                                dofs=(None, 4.0))[:bench.CONFIG4_DATASETS]
     ns = NativeSampler(wl["ptas"], wl["cfgs"], 0)
     ns.alloc(wl["C"], dataset=wl["ds"])
+    ns.set_debug(exact_bdraw="--exact" in sys.argv)
     ns.set_state(**wl["init"])
     ns.sweep(W + K + BURN, seed=SEED, sweep0=0, chain0=0)
     rec = ns.alloc_records(WIN // THIN, keys=("x", "theta"))
@@ -73,6 +84,8 @@ def main():
         b["worst"] = max(b["worst"], r["rhat_max"])
     out = {"schedule": {"warmup": W, "timed": K, "burn": BURN, "window": WIN, "thin": THIN,
                         "seed": SEED, "chains_per_dataset": 64},
+           "start": "bench.workload(4): prior draws, gibbs.py:29-51 latents (vvh17 z = 1)",
+           "b_draw": "exact" if "--exact" in sys.argv else "SVD noise floor (include/gst.h)",
            "by_model": by_model, "datasets": rows}
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
@@ -82,16 +95,19 @@ def main():
                                             "mean_sum_z_end")}))
     print(json.dumps(by_model))
     if worst_npz:
-        # the worst 'beta' and the worst 'uniform' dataset: <stem>_d<dataset>.npz each
+        # the worst 'beta' and the worst 'uniform' dataset, and every --save dataset:
+        # <stem>_d<dataset>.npz each
         stem = worst_npz[:-4] if worst_npz.endswith(".npz") else worst_npz
+        picks = list(save)
         for mdl in ("beta", "uniform"):
             mix = [r for r in rows if r["model"] == mdl]
             if mix:
-                d = mix[0]["dataset"]
-                sel = wl["ds"] == d
-                np.savez(f"{stem}_d{d}.npz", dataset=d, x=x[sel], theta=th[sel],
-                         names=np.array(names), thin=THIN, first_sweep=W + K + BURN)
-                print(f"worst {mdl} dataset", d, "saved to", f"{stem}_d{d}.npz")
+                picks.append(mix[0]["dataset"])
+        for d in dict.fromkeys(picks):
+            sel = wl["ds"] == d
+            np.savez(f"{stem}_d{d}.npz", dataset=d, x=x[sel], theta=th[sel],
+                     names=np.array(names), thin=THIN, first_sweep=W + K + BURN)
+            print("dataset", d, "saved to", f"{stem}_d{d}.npz")
 
 
 if __name__ == "__main__":

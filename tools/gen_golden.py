@@ -411,6 +411,31 @@ def general(niter=12):
                   np.nanmax(out["tape_b_cond"]), file=sys.stderr)
 
 
+def small_ecorr(niter=12):
+    """The general white-noise model with a hyper block the register-resident large-path
+    kernel takes (lg_hyper_reg: nf + n_ecorr <= 62): gdata.multiband with 24 epochs x 3
+    sub-band TOAs (n = 72), 10 red-noise components and 24 ECORR epochs (20 + 24 = 44 hyper
+    columns, m = 58); ``ecb``: per-backend efac / equad / ECORR (P = 8), ``ecn``: one of each
+    (P = 5), as ``general`` (lg_hyper_reg's ECORR branches)."""
+    psr = gdata.multiband(nepochs=24, nsub=3, seed=2443)
+    pta_b = PTA(psr, components=10, efac=(0.2, 10.0), selection="backend",
+                log10_ecorr=(-8.5, -5.0))
+    pta_n = PTA(psr, components=10, efac=(0.2, 10.0), log10_ecorr=(-8.5, -5.0))
+    x0b = [1.1, -6.5, -6.6, 0.9, -6.8, -7.0, 4.33, -14.0]
+    x0n = [1.0, 4.33, -14.0, -6.6, -6.8]
+    for tag, pta_g, x0, models in (("ecb", pta_b, x0b, ("beta", "uniform")),
+                                   ("ecn", pta_n, x0n, ("t", "vvh17"))):
+        np.savez_compressed(os.path.join(OUTDIR, f"{tag}_dataset.npz"),
+                            **dataset_arrays(pta_g, psr))
+        for j, name in enumerate(models):
+            out = run_one(pta_g, name, MODELS[name], seed=7700 + 13 * j + len(tag),
+                          niter=niter, x0=x0)
+            out["model_kw"] = np.array(repr(MODELS[name]))
+            np.savez_compressed(os.path.join(OUTDIR, f"ref_{tag}_{name}_fixed.npz"), **out)
+            print(tag, name, "P", len(x0), "m", pta_g.m, "cond:",
+                  np.nanmax(out["tape_b_cond"]), file=sys.stderr)
+
+
 def mid(niter=12):
     """A mid-size pulsar for the register-resident kernel's wide TOA instances (NS = 6, 8
     slots of 64 TOAs): 130 J1713+0747 epochs x 3 sub-band TOAs (gdata.multiband, one
@@ -449,6 +474,9 @@ def main():
         return
     if "--only-general" in sys.argv:
         general(12)
+        return
+    if "--only-small-ecorr" in sys.argv:
+        small_ecorr(12)
         return
     if "--only-mid" in sys.argv:
         mid(12)
