@@ -287,7 +287,10 @@ __device__ __forceinline__ double wave_max(double v) {
 // the factor over the real columns is below FLOOR_GATE x the largest, b is drawn exactly from
 // Sigma + f I with f = FLOOR_C 2^-52 x the largest pivot; every other draw is the exact one.
 constexpr double FLOOR_GATE = 1e-14;
-constexpr double FLOOR_C = 0.5;
+#ifndef GST_FLOOR_C
+#define GST_FLOOR_C 0.5   // oracle/gibbs_oracle.py FLOOR_C (tools/vvh17_escape.py calibrates it)
+#endif
+constexpr double FLOOR_C = GST_FLOOR_C;
 constexpr int STATUS_FLOOR = 16;
 constexpr int DEBUG_EXACT_BDRAW = 8;
 
@@ -779,6 +782,10 @@ __device__ __forceinline__ void chol_step(double (&L)[SL(MT, 0)], CholCtx& cc,
   // column k+1 starts the paired tail: publish it together with k+2 (pair_handoff)
   constexpr bool TOPAIR = NEXT && K1 >= KP;
   static_assert(!TOPAIR || KK1 == 0, "the paired tail starts at a slot column");
+#ifdef GST_TAILPRIO
+  // experiment: the latency-bound tail issues ahead of the partner wave's trailing updates
+  if constexpr (TOPAIR) __builtin_amdgcn_s_setprio(GST_TAILPRIO);
+#endif
   ColView<MT> nxt, nxt2;
   if constexpr (K1 < MT) {
     // critical path: slot column K1 (holds column k+1).  Its factor a_{8K1+q,k} / a_kk is
@@ -1971,7 +1978,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       // refactor x's Sigma + f I (Gram stage + hyper block; the MH decisions stand)
       if (redraw && !fb && !(st.debug & DEBUG_EXACT_BDRAW)) {
         fshift = floor_shift(f_apr, lane, md.ntm, md.ntm_pad, md.ntm_pad + md.nf);
-        if (fshift != 0.0) {
+        if (__builtin_expect(fshift != 0.0, 0)) {
           status |= STATUS_FLOOR;
           gram_and_tm(xv);
           lnl_hyper(xv, fb);

@@ -29,8 +29,10 @@ from .native import STATE_KEYS, NativeSampler
 class Gibbs:
     def __init__(self, pta, model="gaussian", tdf=4, m=0.01, vary_df=True,
                  theta_prior="beta", vary_alpha=True, alpha=1e10, pspin=None, *,
-                 nchains=1, seed=None, device=0, record_every=1, chunk=512, verbose=False):
-        # gibbs.py:13-51
+                 nchains=1, seed=None, device=0, record_every=1, chunk=512, verbose=False,
+                 exact_bdraw=False):
+        # gibbs.py:13-51.  exact_bdraw: draw b exactly from Sigma also where it is beyond fp64
+        # resolution, instead of at the reference's SVD noise floor (include/gst.h gst_sweep)
         self.pta = pta
         self.mp = m
         self.theta_prior = theta_prior
@@ -59,6 +61,7 @@ class Gibbs:
         cfg = dict(model=model, tdf=tdf, m=m, vary_df=vary_df, theta_prior=theta_prior,
                    vary_alpha=vary_alpha, alpha=alpha, pspin=pspin)
         self._native = NativeSampler(pta, cfg, device)
+        self._native.set_debug(exact_bdraw=exact_bdraw)
         self._native.alloc(C)
 
     # ---- reference attribute names (chain 0 view when nchains == 1) -----------------

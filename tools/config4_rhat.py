@@ -1,6 +1,7 @@
 """Per-dataset convergence of BASELINE config 4.
 
     python tools/config4_rhat.py [out.json] [worst.npz] [--save D1,D2,...] [--exact]
+        [--chains PER_DATASET] [--seed S]
 
 Runs bench.py's config-4 workload (256 run_sims datasets x 64 chains on one GPU) with the
 bench's own schedule (300 warmup sweeps, 1000 timed, 3000 burn-in, then a 5000-sweep window
@@ -32,23 +33,29 @@ W, K, BURN, WIN, THIN, SEED = 300, 1000, 3000, 5000, 5, 20171713
 
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
-    save = []
+    save, chains, seed = [], None, SEED
     for i, a in enumerate(sys.argv):
         if a == "--save":
             save = [int(v) for v in sys.argv[i + 1].split(",")]
             args.remove(sys.argv[i + 1])
+        if a == "--chains":        # chains per dataset (default 64, the bench's)
+            chains = int(sys.argv[i + 1])
+            args.remove(sys.argv[i + 1])
+        if a == "--seed":
+            seed = int(sys.argv[i + 1])
+            args.remove(sys.argv[i + 1])
     dst = args[0] if len(args) > 0 else "config4_rhat.json"
     worst_npz = args[1] if len(args) > 1 else None
-    wl = bench.workload(4, 0, 1, None)
+    wl = bench.workload(4, 0, 1, chains)
     grid = run_sims.build_grid(thetas=(0.05, 0.1, 0.15), realisations=5,
                                dofs=(None, 4.0))[:bench.CONFIG4_DATASETS]
     ns = NativeSampler(wl["ptas"], wl["cfgs"], 0)
     ns.alloc(wl["C"], dataset=wl["ds"])
     ns.set_debug(exact_bdraw="--exact" in sys.argv)
     ns.set_state(**wl["init"])
-    ns.sweep(W + K + BURN, seed=SEED, sweep0=0, chain0=0)
+    ns.sweep(W + K + BURN, seed=seed, sweep0=0, chain0=0)
     rec = ns.alloc_records(WIN // THIN, keys=("x", "theta"))
-    ns.sweep(WIN, records=rec, record_every=THIN, seed=SEED, sweep0=W + K + BURN, chain0=0)
+    ns.sweep(WIN, records=rec, record_every=THIN, seed=seed, sweep0=W + K + BURN, chain0=0)
     x = rec["x"].cpu().numpy()
     th = rec["theta"].cpu().numpy()
     z = ns.get_state()["z"]
@@ -83,7 +90,7 @@ def main():
         b["rhat_gt_1.01"] += int(r["rhat_max"] > 1.01)
         b["worst"] = max(b["worst"], r["rhat_max"])
     out = {"schedule": {"warmup": W, "timed": K, "burn": BURN, "window": WIN, "thin": THIN,
-                        "seed": SEED, "chains_per_dataset": 64},
+                        "seed": seed, "chains_per_dataset": wl["per"]},
            "start": "bench.workload(4): prior draws, gibbs.py:29-51 latents (vvh17 z = 1)",
            "b_draw": "exact" if "--exact" in sys.argv else "SVD noise floor (include/gst.h)",
            "by_model": by_model, "datasets": rows}

@@ -1,6 +1,6 @@
 """Config-4 distributional parity from the same start.
 
-    OPENBLAS_NUM_THREADS=1 python tools/config4_same_start.py oracle D VARIANT OUT.npz
+    OPENBLAS_NUM_THREADS=1 python tools/config4_same_start.py oracle D VARIANT OUT.npz [NCHAINS]
     python tools/config4_same_start.py compare D GPU.npz ORACLE_SVD.npz [ORACLE_FLOOR.npz] OUT.json
 
 ``oracle``: the reference algorithm (oracle/gibbs_oracle.py with gibbs.py's legacy RNG calls)
@@ -11,11 +11,11 @@ latents bench.workload gives them, vvh17 at the reference's z = 1), on the bench
 reference's own b draw (gibbs.py:169-180); ``floor`` the HIP path's rule (exact draw, at the
 SVD noise floor from Sigma + f I; Oracle.floor_shift).  One process per chain slot (8).
 
-``compare``: per-chain modes (vvh17: all-outlier state, window-mean theta >= 1/2; otherwise
-the two clusters of the window-mean log10_equad split at the largest gap), a Fisher exact
-test of the mode counts GPU vs oracle, two-sample KS of the pooled draws within each mode
-and overall, and split-R-hat of each sample.  The GPU draws come from tools/config4_rhat.py
-(``--save D1,D2,...``).
+``compare``: per-chain modes (the two clusters of the window-mean log10_equad split at the
+largest gap; vvh17's all-outlier state counted too), a Fisher exact test of the mode counts
+GPU vs oracle, KS and Welch t tests of the per-chain window means within each mode (the
+chains are the independent samples), and split-R-hat of each sample.  The GPU draws come
+from tools/config4_rhat.py (``--save D1,D2,...``).
 """
 import json
 import os
@@ -40,13 +40,13 @@ def _entry(d):
 
 
 def _chain(args):
-    d, variant, c = args
+    d, variant, c, nch = args
     warnings.simplefilter("ignore")
     from gibbs_student_t_amd import run_sims
     from oracle.gibbs_oracle import ChainState, LegacyNumpyVariates, Oracle, OutlierModel
     e = _entry(d)
     n = e.pta.n
-    init = run_sims.initial_state(e, CHAINS, d * CHAINS, SEED0, n, "reference")
+    init = run_sims.initial_state(e, nch, d * CHAINS, SEED0, n, "reference")
     orc = Oracle(e.pta, OutlierModel(**e.cfg))
     st = ChainState(b=init["b"][c].copy(), z=init["z"][c, :n].copy(),
                     alpha=init["alpha"][c, :n].copy(), pout=init["pout"][c, :n].copy(),
@@ -63,23 +63,16 @@ def _chain(args):
     return np.asarray(rec), float(np.sum(st.z))
 
 
-def run_oracle(d, variant, out):
+def run_oracle(d, variant, out, nch=CHAINS):
+    """Chains 0..63 start exactly as the GPU's; NCHAINS > 64 adds further prior draws."""
     with Pool(8) as pool:
-        res = pool.map(_chain, [(d, variant, c) for c in range(CHAINS)], chunksize=1)
+        res = pool.map(_chain, [(d, variant, c, nch) for c in range(nch)], chunksize=1)
     e = _entry(d)
     names = [p.name.split("_", 1)[1] for p in e.pta.params]
     np.savez(out, dataset=d, variant=variant, x=np.stack([r[0][:, :-1] for r in res]),
              theta=np.stack([r[0][:, -1] for r in res]),
              sum_z_end=np.array([r[1] for r in res]), names=np.array(names), thin=THIN,
              first_sweep=BURN)
-
-
-def _modes(model, x, theta, names):
-    """Mode label per chain (0/1) and what splits them."""
-    if model == "vvh17":
-        return (theta.mean(1) >= 0.5).astype(int), "window-mean theta >= 1/2 (all-outlier)"
-    j = [i for i, nm in enumerate(names) if "equad" in nm][0]
-    return None, j
 
 
 def compare(d, gpu_f, svd_f, floor_f, out):
@@ -94,41 +87,41 @@ def compare(d, gpu_f, svd_f, floor_f, out):
            "n": e.pta.n, "schedule": {"burn": BURN, "window": WIN, "thin": THIN},
            "start": "run_sims.initial_state(..., 'reference'): the GPU chains' own states",
            "samples": {}}
-    # modes: vvh17 -> trapped or not; else split the pooled chain means of log10_equad at
-    # their largest gap (bimodal beta posteriors: outliers flagged vs absorbed in EQUAD)
-    if e.model == "vvh17":
-        lab = {k: (s["theta"].mean(1) >= 0.5).astype(int) for k, s in samples.items()}
-        res["mode_rule"] = "window-mean theta >= 1/2 (all-outlier state)"
-    else:
-        j = [i for i, nm in enumerate(names) if "equad" in nm][0]
-        cm = np.sort(np.concatenate([s["x"][:, :, j].mean(1) for s in samples.values()]))
-        gaps = np.diff(cm)
-        g = int(np.argmax(gaps))
-        cut = 0.5 * (cm[g] + cm[g + 1])
-        res["mode_rule"] = f"window-mean {names[j]} > {cut:.4f} (largest gap {gaps[g]:.3f})"
-        lab = {k: (s["x"][:, :, j].mean(1) > cut).astype(int) for k, s in samples.items()}
+    # modes: the pooled chain means of log10_equad split at their largest gap (the bimodal
+    # posteriors of config 4: outliers flagged vs absorbed into a large EQUAD); vvh17's
+    # all-outlier state (window-mean theta >= 1/2) is counted separately
+    j = [i for i, nm in enumerate(names) if "equad" in nm][0]
+    cm = np.sort(np.concatenate([s["x"][:, :, j].mean(1) for s in samples.values()]))
+    gaps = np.diff(cm)
+    g = int(np.argmax(gaps))
+    cut = 0.5 * (cm[g] + cm[g + 1])
+    res["mode_rule"] = f"window-mean {names[j]} > {cut:.4f} (largest gap {gaps[g]:.3f})"
+    lab = {k: (s["x"][:, :, j].mean(1) > cut).astype(int) for k, s in samples.items()}
     series = lambda s: [(nm, s["x"][:, :, i]) for i, nm in enumerate(names)] + \
         [("theta", s["theta"])]
     for k, s in samples.items():
-        row = {"mode1_chains": int(lab[k].sum()), "chains": int(len(lab[k])), "rhat": {}}
+        row = {"mode1_chains": int(lab[k].sum()), "chains": int(len(lab[k])),
+               "all_outlier_chains": int(np.sum(s["theta"].mean(1) >= 0.5)), "rhat": {}}
         for nm, v in series(s):
             row["rhat"][nm] = float(diag.ess_rhat(v)[1])
         res["samples"][k] = row
+    # Within a mode the draws of a chain are autocorrelated (a pooled KS of 64 x 1000 draws
+    # rejects even between two runs of the reference algorithm), so the chains are the
+    # independent samples: KS and Welch t on the per-chain window means, per mode.
     for k in samples:
         if k == "oracle_svd":
             continue
         a, b = lab[k], lab["oracle_svd"]
         table = [[int(a.sum()), int(len(a) - a.sum())], [int(b.sum()), int(len(b) - b.sum())]]
         cmp = {"mode_table": table, "fisher_p": float(scipy.stats.fisher_exact(table)[1]),
-               "ks_overall": {}, "ks_in_mode": {}}
-        for (nm, g), (_, r) in zip(series(samples[k]), series(samples["oracle_svd"])):
-            cmp["ks_overall"][nm] = float(scipy.stats.ks_2samp(g[:, ::2].ravel(),
-                                                               r[:, ::2].ravel()).pvalue)
+               "chain_means_in_mode": {}}
+        for (nm, gx), (_, rx) in zip(series(samples[k]), series(samples["oracle_svd"])):
             for m in (0, 1):
-                gm, rm = g[a == m], r[b == m]
-                if len(gm) >= 2 and len(rm) >= 2:
-                    cmp["ks_in_mode"].setdefault(f"mode{m}", {})[nm] = float(
-                        scipy.stats.ks_2samp(gm[:, ::2].ravel(), rm[:, ::2].ravel()).pvalue)
+                gm, rm = gx[a == m].mean(1), rx[b == m].mean(1)
+                if len(gm) >= 3 and len(rm) >= 3:
+                    cmp["chain_means_in_mode"].setdefault(f"mode{m}", {})[nm] = {
+                        "ks_p": float(scipy.stats.ks_2samp(gm, rm).pvalue),
+                        "welch_p": float(scipy.stats.ttest_ind(gm, rm, equal_var=False).pvalue)}
         res[f"{k}_vs_oracle_svd"] = cmp
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
@@ -137,7 +130,8 @@ def compare(d, gpu_f, svd_f, floor_f, out):
 
 def main():
     if sys.argv[1] == "oracle":
-        run_oracle(int(sys.argv[2]), sys.argv[3], sys.argv[4])
+        run_oracle(int(sys.argv[2]), sys.argv[3], sys.argv[4],
+                   int(sys.argv[5]) if len(sys.argv) > 5 else CHAINS)
     elif sys.argv[1] == "compare":
         rest = sys.argv[3:]
         floor_f = rest[2] if len(rest) == 4 else None
