@@ -593,10 +593,14 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
   const int nsb = (h.mp / 16 + 3) / 4;
   const int npairs = nsb * (nsb + 1) / 2;
   const bool small_toa = ys <= gst::TBLK_SMALL_NPAD;
-  // hyper blocks of up to HR_COLS (62) columns: one wave per chain, register-resident elimination
-  bool hyper_reg = !(cx->debug & GST_DEBUG_LARGE_HYPER);
-  for (const gst::DevModel& hm : cx->hmd) hyper_reg = hyper_reg && hm.nf + hm.nec <= gst::HR_COLS;
-  const dim3 g_hr((C + gst::HR_WPB - 1) / gst::HR_WPB), b_hr(64 * gst::HR_WPB);
+  // hyper blocks of up to HR_COLS (62) / HR_COLS_WIDE (126) columns: one wave per chain,
+  // register-resident elimination (lg_hyper_reg<8> / <16>); larger ones: lg_hyper (LDS)
+  int hcols = 0;
+  for (const gst::DevModel& hm : cx->hmd) hcols = std::max(hcols, hm.nf + hm.nec);
+  int hr_mt = hcols <= gst::HR_COLS ? 8 : (hcols <= gst::HR_COLS_WIDE ? 16 : 0);
+  if (cx->debug & GST_DEBUG_LARGE_HYPER) hr_mt = 0;
+  const int hr_wpb = hr_mt == 16 ? gst::HR<16>::WPB : gst::HR<8>::WPB;
+  const dim3 g_hr((C + hr_wpb - 1) / hr_wpb), b_hr(64 * hr_wpb);
   // Grams of at most GS_NTMAX 16-column tiles: one wave per chain (lg_gram_small<NT>)
   int gram_small = h.mp / 16;
   for (const gst::DevModel& hm : cx->hmd)
@@ -637,8 +641,10 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
       if (ev_mark(cx, GST_K_GRAM, st, false)) return -1;
       LG_LAUNCH(GST_K_TMELIM, gst::lg_tmelim, g_chain, b_chain, cx->lds_tm);
       if (!(mask & GST_STAGE_GRAM)) {   // timing diagnostic: Gram + TM elimination only
-        if (hyper_reg)
-          LG_LAUNCH(GST_K_HYPER, gst::lg_hyper_reg, g_hr, b_hr, 0);
+        if (hr_mt == 8)
+          LG_LAUNCH(GST_K_HYPER, gst::lg_hyper_reg<8>, g_hr, b_hr, 0);
+        else if (hr_mt == 16)
+          LG_LAUNCH(GST_K_HYPER, gst::lg_hyper_reg<16>, g_hr, b_hr, 0);
         else
           LG_LAUNCH(GST_K_HYPER, gst::lg_hyper, g_chain, b_chain, cx->lds_hyper);
         if (eval_only) break;
@@ -648,8 +654,10 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
           // returns at once (SC_FLOOR == 0)
           a.floor_pass = 1;
           LG_LAUNCH(GST_K_TMELIM, gst::lg_tmelim, g_chain, b_chain, cx->lds_tm);
-          if (hyper_reg)
-            LG_LAUNCH(GST_K_HYPER, gst::lg_hyper_reg, g_hr, b_hr, 0);
+          if (hr_mt == 8)
+            LG_LAUNCH(GST_K_HYPER, gst::lg_hyper_reg<8>, g_hr, b_hr, 0);
+          else if (hr_mt == 16)
+            LG_LAUNCH(GST_K_HYPER, gst::lg_hyper_reg<16>, g_hr, b_hr, 0);
           else
             LG_LAUNCH(GST_K_HYPER, gst::lg_hyper, g_chain, b_chain, cx->lds_hyper);
           a.floor_pass = 0;

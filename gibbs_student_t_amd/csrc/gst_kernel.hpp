@@ -288,7 +288,7 @@ __device__ __forceinline__ double wave_max(double v) {
 // Sigma + f I with f = FLOOR_C 2^-52 x the largest pivot; every other draw is the exact one.
 constexpr double FLOOR_GATE = 1e-14;
 #ifndef GST_FLOOR_C
-#define GST_FLOOR_C 0.5   // oracle/gibbs_oracle.py FLOOR_C (tools/vvh17_escape.py calibrates it)
+#define GST_FLOOR_C 0.75  // oracle/gibbs_oracle.py FLOOR_C (tools/vvh17_escape.py calibrates it)
 #endif
 constexpr double FLOOR_C = GST_FLOOR_C;
 constexpr int STATUS_FLOOR = 16;

@@ -997,39 +997,48 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
 }
 
 // ------------------------------------------------------------------------------------
-// hyper, register-resident (hyper block of at most HR_COLS = 62 columns): one wave per chain runs
-// lg_hyper's MH with the persistent kernel's elimination (gst_kernel.hpp chol_range: 8x8-
-// cyclic register layout, one published column per LDS hand-off) instead of an LDS
-// factorisation with a workgroup barrier per column.  Internal order: the nf hyper columns,
-// unit-prior dummies up to HR_RA (exact no-ops: zero coupling, pivot 1), the augmented row
-// at HR_RA, one zero pad row.  Same variates, MH decisions and outputs (x, status, v's Fourier block, the
-// redraw flags) as lg_hyper; the likelihood sums run in the persistent kernel's order.
+// hyper, register-resident (hyper blocks of at most 62 / 126 columns, MT = 8 / 16): one wave
+// per chain runs lg_hyper's MH with the persistent kernel's elimination (gst_kernel.hpp
+// chol_range: 8x8-cyclic register layout, one published column per LDS hand-off) instead of
+// an LDS factorisation with a workgroup barrier per column.  Internal order: the nf hyper
+// columns, unit-prior dummies up to RA (exact no-ops: zero coupling, pivot 1), the augmented
+// row at RA, one zero pad row.  Same variates, MH decisions and outputs (x, status, v's
+// Fourier block, the redraw flags) as lg_hyper; the likelihood sums run in the persistent
+// kernel's order.  MT = 16 (config 5's 121-row block, the 80-column ECORR models): 272
+// registers of factor per lane, so no paired tail (its second column view would spill) and
+// two chains per workgroup (S0 is 68 KB of LDS per chain).
 // ------------------------------------------------------------------------------------
-constexpr int HR_MT = 8;                          // 64 internal rows
-constexpr int HR_RA = 8 * HR_MT - 2;              // augmented row (the paired tail covers an
-                                                  // even number of columns from slot KP)
-constexpr int HR_COLS = HR_RA;                    // hyper columns it takes (nf + nec)
-constexpr int HR_WPB = 4;                         // chains (waves) per workgroup
-constexpr int HR_S0 = 64 * SL(HR_MT, 0);          // S0 [slot][lane]
-constexpr int HR_LDS = HR_S0 + 8 * HR_MT /*colq*/ + 8 * HR_MT /*junk*/ +
-                       8 * pair_pw(HR_MT) /*colq2*/ + 64 /*phi^-1*/ + 4 * NHYPER /*mhv*/ +
-                       64 /*rhs*/;
+template <int MT>
+struct HR {
+  static constexpr int RA = 8 * MT - 2;        // augmented row (the paired tail covers an
+                                               // even number of columns from slot KP)
+  static constexpr int WPB = MT <= 8 ? 4 : 2;  // chains (waves) per workgroup
+  static constexpr int KP = MT <= 8 ? kp_for(1) : MT;
+  static constexpr int NCS = (8 * MT + 63) / 64;   // hyper columns per lane (64 sl + lane)
+  static constexpr int S0 = 64 * SL(MT, 0);        // S0 [slot][lane]
+  static constexpr int LDS = S0 + 8 * MT /*colq*/ + 8 * MT /*junk*/ + 8 * pair_pw(MT) /*colq2*/ +
+                             64 * NCS /*phi^-1*/ + 4 * NHYPER /*mhv*/ + 64 * NCS /*rhs*/;
+};
+constexpr int HR_COLS = HR<8>::RA;        // hyper columns (nf + nec) lg_hyper_reg<8> takes
+constexpr int HR_COLS_WIDE = HR<16>::RA;  // ... and lg_hyper_reg<16>
 
-__global__ void __launch_bounds__(64 * HR_WPB) lg_hyper_reg(const DevModel* __restrict__ mds,
-                                                              LArgs a) {
-  constexpr int MT = HR_MT, RA = HR_RA, NSL = SL(MT, 0);
-  __shared__ double smem[HR_WPB][HR_LDS];
+template <int MT>
+__global__ void __launch_bounds__(64 * HR<MT>::WPB) lg_hyper_reg(const DevModel* __restrict__ mds,
+                                                                   LArgs a) {
+  using H = HR<MT>;
+  constexpr int RA = H::RA, NSL = SL(MT, 0), NCS = H::NCS, WPB = H::WPB;
+  __shared__ double smem[WPB][H::LDS];
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int c = blockIdx.x * HR_WPB + wv;
+  const int c = blockIdx.x * WPB + wv;
   if (c >= a.C) return;
   const DevModel& md = mds[ds_of(a, c)];
   double* S0R = smem[wv];
-  double* colq = S0R + HR_S0;
+  double* colq = S0R + H::S0;
   double* junk = colq + 8 * MT;
   double* colq2 = junk + 8 * MT;
   double* ph = colq2 + 8 * pair_pw(MT);
-  double* mhv = ph + 64;
+  double* mhv = ph + 64 * NCS;
   double* rhs = mhv + 4 * NHYPER;
   const int p = lane >> 3, q = lane & 7;
   const int nf = md.nf + md.nec, nfr = md.nf, K0 = md.ntm_pad, mp = md.mp;
@@ -1071,17 +1080,21 @@ __global__ void __launch_bounds__(64 * HR_WPB) lg_hyper_reg(const DevModel* __re
     const double lA = xget(xq, md.idx_logA);
     const double g = xget(xq, md.idx_gamma);
     const double lc = 2.0 * lA * 2.302585092994045684 - md.log_12pi2 + (g - 3.0) * md.log_fyr;
-    double pv = 0.0;                    // phi^-1 of internal column `lane` (0: none)
-    if (lane < nfr) {
-      pv = exp(-(lc - g * md.lfreq[lane] + md.ldf[lane])) + fsh;
-    } else if (lane < nf) {
-      const int b = md.ecb[lane - nfr];
-      int pi = md.ecorr_b[0];
 #pragma unroll
-      for (int j = 1; j < NBMAX; ++j) pi = (b == j) ? md.ecorr_b[j] : pi;
-      pv = exp(-2.0 * xget(xq, pi) * 2.302585092994045684) + fsh;
+    for (int cs = 0; cs < NCS; ++cs) {
+      const int jc = 64 * cs + lane;
+      double pv = 0.0;                  // phi^-1 of internal column jc (0: none)
+      if (jc < nfr) {
+        pv = exp(-(lc - g * md.lfreq[jc] + md.ldf[jc])) + fsh;
+      } else if (jc < nf) {
+        const int b = md.ecb[jc - nfr];
+        int pi = md.ecorr_b[0];
+#pragma unroll
+        for (int j = 1; j < NBMAX; ++j) pi = (b == j) ? md.ecorr_b[j] : pi;
+        pv = exp(-2.0 * xget(xq, pi) * 2.302585092994045684) + fsh;
+      }
+      ph[jc] = pv;
     }
-    ph[lane] = pv;
     double logdet_phi = ((double)nfr * lc - g * md.sum_lfreq + md.sum_ldf) + md.logdet_phi_tm;
     for (int b = 0; b < md.nb; ++b)
       if (md.ec_count[b] > 0.0)
@@ -1096,11 +1109,14 @@ __global__ void __launch_bounds__(64 * HR_WPB) lg_hyper_reg(const DevModel* __re
         L[SL(r, s2)] = v;
       }
     CholCtx cc{colq, junk, colq2, lane, p, q, RA, 1.0, 0.0, 0, 0, {1.0, 1.0}, {0.0, 0.0}};
-    chol_range<MT, 0, RA, kp_for(1)>(L, cc);
+    chol_range<MT, 0, RA, H::KP>(L, cc);
     chol_harvest<MT, 0, RA, RA>(L, cc);
     chol_stats<0, RA>(cc);
-    apr[0] = cc.apr[0];
-    zr[0] = cc.zr[0];
+#pragma unroll
+    for (int cs = 0; cs < NCS; ++cs) {
+      apr[cs] = cc.apr[cs];
+      zr[cs] = cc.zr[cs];
+    }
     failed = cc.fail | fail_tm;
     if (failed) return -INFINITY;
     const double ld = log(cc.mant) + (double)cc.expo * 0.693147180559945309417;
@@ -1174,7 +1190,7 @@ __global__ void __launch_bounds__(64 * HR_WPB) lg_hyper_reg(const DevModel* __re
   double fs = 0.0;
   if (!a.floor_pass && redraw && !fb && !(a.st.debug & DEBUG_EXACT_BDRAW)) {
     double mn, mx;
-    const double ap[2] = {apr[0], 1.0};
+    const double ap[2] = {apr[0], NCS > 1 ? apr[1] : 1.0};
     pivot_range(ap, lane, 0, 0, nf, mn, mx);
     fs = floor_of(fmin(mn, sc[SC_TMPMIN]), fmax(mx, sc[SC_TMPMAX]));
   }
@@ -1188,18 +1204,22 @@ __global__ void __launch_bounds__(64 * HR_WPB) lg_hyper_reg(const DevModel* __re
   }
   if (!redraw || fb || fs > 0.0) return;   // fs > 0: the floor pass draws b
   // b draw, hyper block (lg_hyper's back substitution): the raw factor goes to the S0 region
-  // ([slot][lane]: a_ik at 64 SL(i/8, k/8) + 8 (i%8) + k%8); lane k owns column k
+  // ([slot][lane]: a_ik at 64 SL(i/8, k/8) + 8 (i%8) + k%8); lane owns columns lane + 64 cs
 #pragma unroll
   for (int sl = 0; sl < NSL; ++sl) S0R[64 * sl + lane] = L[sl];
   lds_order();
   auto aik = [&](int i, int k) __attribute__((always_inline)) { return S0R[64 * SL(i >> 3, k >> 3) + 8 * (i & 7) + (k & 7)]; };
-  const int k = lane;
-  const bool kin = k < nf;
-  const double akk = apr[0];            // pivot of column `lane` (chol_harvest)
-  const double yk = kin ? rsqrt_nr(akk) : 0.0;
-  double w = 0.0;
+  double yk[NCS], w[NCS], acc[NCS];       // acc_k = sum_{i > k} a_ik v_i
+#pragma unroll
+  for (int cs = 0; cs < NCS; ++cs) {
+    const int k = 64 * cs + lane;
+    yk[cs] = k < nf ? rsqrt_nr(apr[cs]) : 0.0;   // apr: pivot of column k (chol_harvest)
+    w[cs] = 0.0;
+    acc[cs] = 0.0;
+  }
   if (tp) {
-    rhs[k] = 0.0;
+#pragma unroll
+    for (int cs = 0; cs < NCS; ++cs) rhs[64 * cs + lane] = 0.0;
     lds_order();
     for (int j = lane; j < md.m; j += 64) {
       const int ii = md.ref2int[j] - K0;
@@ -1207,20 +1227,37 @@ __global__ void __launch_bounds__(64 * HR_WPB) lg_hyper_reg(const DevModel* __re
     }
     lds_order();
     // eta_k = y_k sum_{i >= k} a_ik Delta_i (so that L^-T eta = Delta)
-    double sacc = 0.0;
-    if (kin)
-      for (int i = k; i < nf; ++i) sacc += aik(i, k) * rhs[i];
-    w = (zr[0] + sacc) * yk;
-  } else if (kin) {
-    w = zr[0] * yk + normal_k(rng, (uint32_t)(K0 + k), TAG_BDRAW);
+#pragma unroll
+    for (int cs = 0; cs < NCS; ++cs) {
+      const int k = 64 * cs + lane;
+      double sacc = 0.0;
+      if (k < nf)
+        for (int i = k; i < nf; ++i) sacc += aik(i, k) * rhs[i];
+      w[cs] = (zr[cs] + sacc) * yk[cs];
+    }
+  } else {
+#pragma unroll
+    for (int cs = 0; cs < NCS; ++cs) {
+      const int k = 64 * cs + lane;
+      if (k < nf) w[cs] = zr[cs] * yk[cs] + normal_k(rng, (uint32_t)(K0 + k), TAG_BDRAW);
+    }
   }
   double* vF = a.s.v + (size_t)c * mp + K0;
-  double acc = 0.0;                     // acc_k = sum_{i > k} a_ik v_i
   for (int i = nf - 1; i >= 0; --i) {
-    const double yi = rdlane(yk, i), wi = rdlane(w, i), ai = rdlane(acc, i);
+    double ys = yk[0], ws = w[0], as = acc[0];
+    if (NCS > 1 && i >= 64) {
+      ys = yk[NCS - 1];
+      ws = w[NCS - 1];
+      as = acc[NCS - 1];
+    }
+    const double yi = rdlane(ys, i & 63), wi = rdlane(ws, i & 63), ai = rdlane(as, i & 63);
     const double vi = (wi - yi * ai) * yi;
     if (lane == 0) vF[i] = vi;
-    if (k < i) acc += aik(i, k) * vi;
+#pragma unroll
+    for (int cs = 0; cs < NCS; ++cs) {
+      const int k = 64 * cs + lane;
+      if (k < i) acc[cs] += aik(i, k) * vi;
+    }
   }
 }
 

@@ -191,7 +191,7 @@ int gst_model_info(void* ctx, int* ndatasets, int* nmax, int* tape_stride);
  * Sigma is beyond fp64 resolution -- its smallest LDL^T pivot (timing-model-first order, real
  * columns) below 1e-14 of its largest, p_max.  There the reference's sl.svd returns the small
  * eigenvalues at LAPACK's rounding floor (~eps x s_max) and its draw is that of Sigma + f I;
- * this path draws from Sigma + f I with f = 0.5 x 2^-52 p_max (and flags status & 16), which
+ * this path draws from Sigma + f I with f = 0.75 x 2^-52 p_max (and flags status & 16), which
  * reproduces the reference's escape from vvh17's all-outlier start.
  * GST_DEBUG_EXACT_BDRAW turns the floor off. */
 int gst_sweep(void* ctx, const gst_state* state, const gst_records* rec,

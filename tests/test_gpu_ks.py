@@ -55,6 +55,12 @@ def test_posterior_marginals_match_reference(model):
     burn, thin = int(ref["burn"]), 2 * int(ref["thin"])
     rx, rth, rnu = ref["x"][:, ::2], ref["theta"][:, ::2], ref["nu"][:, ::2]
     pta = load_dataset()
+    if model == "vvh17":
+        # from the reference's all-outlier start a few chains escape only after ~500 sweeps
+        # (as the reference's do, test_vvh17_reference_start_escapes_as_the_reference); this
+        # 3000-sweep window must start after they have mixed (slow gamma), where the
+        # reference's 8 x 40000 draws are dominated by converged sweeps
+        burn = 5000
     C, S = 1024, burn + 60 * thin
     ns = NativeSampler(pta, MODELS[model], 0)
     ns.alloc(C)

@@ -71,18 +71,26 @@ def test_register_hyper_matches_lds_hyper(pta):
     assert np.all(np.abs(h_a - h_b) <= 1e-11 * np.abs(h_b)), np.max(np.abs(h_a - h_b) / np.abs(h_b))
     for k in ("x", "z", "nu"):
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
-    for k in ("b", "alpha", "pout", "theta"):
+    # b normwise per chain-sweep (its small components carry cond(Sigma) x eps of the two
+    # eliminations' rounding: the scaled fixture's 120-column block reaches cond ~ 1e10)
+    eb = np.linalg.norm(a["b"] - b["b"], axis=-1) / np.maximum(np.linalg.norm(b["b"], axis=-1),
+                                                                1e-300)
+    assert np.all(eb <= 1e-8), ("b", eb.max())
+    for k in ("alpha", "pout", "theta"):
         d = np.abs(a[k] - b[k])
         assert np.all(d <= 1e-8 * np.maximum(np.abs(b[k]), 1e-300) + 1e-300), (k, d.max())
 
 
 @pytest.mark.parametrize("name", ["ecb_beta_fixed", "ecb_uniform_fixed", "ecn_t_fixed",
-                                  "ecn_vvh17_fixed"])
+                                  "ecn_vvh17_fixed", "mb_beta_fixed", "mbn_vvh17_fixed",
+                                  "scaled_beta_fixed"])
 def test_register_hyper_matches_lds_hyper_ecorr(name):
     """lg_hyper_reg's ECORR and per-backend branches (phi^-1 of the ECORR columns from their
     backend's log10_ecorr, the ECORR log|phi| term, the b draw over ECORR columns) against
-    lg_hyper on reference fixtures with 44 hyper columns (20 Fourier + 24 ECORR epochs);
-    their parity with the reference itself is test_gpu_parity.py's large-path replays."""
+    lg_hyper on reference fixtures with 44 hyper columns (20 Fourier + 24 ECORR epochs:
+    lg_hyper_reg<8>) and 80 / 120 (mb: 20 + 60 ECORR; scaled: 60 components:
+    lg_hyper_reg<16>, two columns per lane); their parity with the reference itself is
+    test_gpu_parity.py's large-path replays."""
     if not torch.cuda.is_available():
         pytest.skip("needs a HIP device")
     from golden_io import load_ref, sweep_state
@@ -108,6 +116,11 @@ def test_register_hyper_matches_lds_hyper_ecorr(name):
     np.testing.assert_array_equal(a["status"], b["status"])
     for k in ("x", "z", "nu"):
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
-    for k in ("b", "alpha", "pout", "theta"):
+    # b normwise per chain-sweep (its small components carry cond(Sigma) x eps of the two
+    # eliminations' rounding: the scaled fixture's 120-column block reaches cond ~ 1e10)
+    eb = np.linalg.norm(a["b"] - b["b"], axis=-1) / np.maximum(np.linalg.norm(b["b"], axis=-1),
+                                                                1e-300)
+    assert np.all(eb <= 1e-8), ("b", eb.max())
+    for k in ("alpha", "pout", "theta"):
         d = np.abs(a[k] - b[k])
         assert np.all(d <= 1e-8 * np.maximum(np.abs(b[k]), 1e-300) + 1e-300), (k, d.max())

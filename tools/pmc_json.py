@@ -1,6 +1,6 @@
-"""profiles/r3_pmc_config2.json from the PMC passes of tools/profile_r3.sh.
+"""profiles/<round>_pmc_config2.json from the PMC passes of tools/profile.sh.
 
-    python tools/r3/pmc_json.py gpurun_out/prof_r3 200 2048 > profiles/r3_pmc_config2.json
+    python tools/pmc_json.py gpurun_out/prof_r4 200 2048 > profiles/r4_pmc_config2.json
 
 The timed dispatch is the last gst_sweep_kernel launch of each pass (bench.py with
 --ess-window 0 --no-stage-costs: the warmup launch, then the timed launch).  HBM bytes follow

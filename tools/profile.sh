@@ -1,9 +1,10 @@
 #!/bin/bash
-# Round-3 profile of the current build:   gpurun -- 'bash tools/profile_r3.sh'
+# Profile of the current build:   gpurun -- 'ROUND=r4 bash tools/profile.sh'
 # bench lines (driver command, default, configs 3/4/5), rocprofv3 kernel stats of the
-# 500-sweep headline run, PMC passes of config 2 and of config 5 (one counter group per run).
+# 500-sweep headline run, PMC passes of config 2 and of config 5 (one counter group per run);
+# then: python tools/pmc_json.py gpurun_out/prof_$ROUND 200 2048 > profiles/${ROUND}_pmc_config2.json
 source tools/gpu_step.sh
-O=gpurun_out/prof_r3; mkdir -p $O
+O=gpurun_out/prof_${ROUND:-r4}; mkdir -p $O
 step 300 $O/bench_driver.json python bench.py --steps 20 --warmup 5
 B="python bench.py --no-cpu-baseline"
 step 300 $O/bench_s500.json $B --steps 500 --warmup 100

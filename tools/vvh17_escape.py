@@ -13,7 +13,7 @@ the same prior draws with one b-draw rule:
 * ``svd``: the reference's own draw (u (u^T d / s) + u s^-1/2 xi);
 * ``exact``: the exact Cholesky draw from Sigma;
 * ``floorC``: the HIP path's rule (oracle ``Oracle.floor_shift``): exact draw from
-  Sigma + f I with f = C x 2^-52 x the largest pivot (C = 0.5) when the smallest pivot is below
+  Sigma + f I with f = C x 2^-52 x the largest pivot (C = 0.75) when the smallest pivot is below
   1e-14 of it.
 
 Prints and writes the escape sweep (first sweep whose z has sum < n / 2) per seed, the
@@ -60,7 +60,7 @@ def run_one(args):
     pta, cfg = _setup(dataset)
     orc = go.Oracle(pta, cfg)
     mean = "svd"
-    go.FLOOR_GATE, go.FLOOR_C = 1e-14, 0.5      # pool workers are reused: reset every job
+    go.FLOOR_GATE, go.FLOOR_C = 1e-14, 0.75     # pool workers are reused: reset every job
     if variant == "exact":
         go.FLOOR_GATE = 0.0
         mean = "floor"
