@@ -782,10 +782,6 @@ __device__ __forceinline__ void chol_step(double (&L)[SL(MT, 0)], CholCtx& cc,
   // column k+1 starts the paired tail: publish it together with k+2 (pair_handoff)
   constexpr bool TOPAIR = NEXT && K1 >= KP;
   static_assert(!TOPAIR || KK1 == 0, "the paired tail starts at a slot column");
-#ifdef GST_TAILPRIO
-  // experiment: the latency-bound tail issues ahead of the partner wave's trailing updates
-  if constexpr (TOPAIR) __builtin_amdgcn_s_setprio(GST_TAILPRIO);
-#endif
   ColView<MT> nxt, nxt2;
   if constexpr (K1 < MT) {
     // critical path: slot column K1 (holds column k+1).  Its factor a_{8K1+q,k} / a_kk is
