@@ -633,15 +633,17 @@ def main():
             # timed per launch by HIP events
             toa_ms = ktimes["white"][0] + ktimes["toa"][0]
             gbs = toa_pass_bytes(n_eff) * C * K / (toa_ms * 1e-3) / 1e9
-            toa = {"kernels": "lg_white + lg_toa (HIP events per launch)", "GBps": gbs,
-                   "hbm_frac": gbs / HBM_PEAK_GBS,
-                   "bytes_per_chain_sweep": toa_pass_bytes(n_eff)}
+            toa = {"kernels": "lg_white + lg_toa (HIP events per launch)",
+                   "algorithmic_GBps": gbs,
+                   "bytes_per_chain_sweep": toa_pass_bytes(n_eff),
+                   "what": "SURVEY.md 8d's algorithmic bytes over the kernels' time, not an HBM "
+                           "measurement (HBM bytes: the PMC passes in profiles/*_pmc_config5.json)"}
         traffic, traffic_src = None, None
         # HBM bytes per chain-sweep of the persistent kernel, PMC (FETCH_SIZE x 2 +
         # WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction) at 2048 chains: a rocprofv3
         # --pmc pass of this same command, stored under profiles/ -- NOT measured in this
         # run (counters need their own profiler pass); the newest profile is used
-        for pf in ("r3_pmc_config2.json", "r2b_pmc_config2.json"):
+        for pf in ("r4_pmc_config2.json", "r3_pmc_config2.json", "r2b_pmc_config2.json"):
             pmc = os.path.join(ROOT, "profiles", pf)
             if os.path.exists(pmc) and args.config == 2 and not args.stub:
                 try:
@@ -653,7 +655,7 @@ def main():
                     break
                 except Exception:
                     traffic = None
-        for pf in ("r3_pmc_config5.json", "pmc_config5.json"):
+        for pf in ("r4_pmc_config5.json", "r3_pmc_config5.json", "pmc_config5.json"):
             pmc5 = os.path.join(ROOT, "profiles", pf)
             if large and args.config == 5 and os.path.exists(pmc5):
                 try:   # HBM bytes per Gram launch (PMC passes of tools/run_large.py, same shape)
@@ -672,8 +674,11 @@ def main():
             gbs = toa_pass_bytes(n_eff) * C / (t_toa * 1e-3) / 1e9
             toa = {"kernels": "gst_sweep_kernel, stage-masked launch (white MH + theta/z/alpha/"
                               "nu) minus an empty launch, HIP events, this run",
-                   "ms_per_sweep": t_toa, "GBps": gbs, "hbm_frac": gbs / HBM_PEAK_GBS,
-                   "bytes_per_chain_sweep": toa_pass_bytes(n_eff)}
+                   "ms_per_sweep": t_toa, "onchip_algorithmic_GBps": gbs,
+                   "bytes_per_chain_sweep": toa_pass_bytes(n_eff),
+                   "what": "SURVEY.md 8d's algorithmic bytes over the stage's time; at these "
+                           "sizes they are register / L2-resident, so this is NOT an HBM "
+                           "rate (the kernel's HBM bytes: roofline.traffic, PMC)"}
             g_alg = n_eff * (m + 1) * (m + 2)
             g_mf = gram_mfma_flops(int(n), pta0.nfourier, pta0.ntm)
             h_exe = exe["gram"] + exe["tm_elim"] + exe["hyper_chol"]

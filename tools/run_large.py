@@ -38,7 +38,8 @@ def main():
     print(f"path={ns.path} C={C} S={S} {dt / S * 1e3:.1f} ms/sweep")
     for k, (ms, nl) in kt.items():
         print(f"  {k:8s} {ms / max(1, S):9.3f} ms/sweep  ({nl} launches)")
-    assert np.all(ns.get_state()["status"] == 0)
+    # status bit 4 (16): b drawn at the SVD noise floor (prior draws near log10_A = -18)
+    assert np.all((ns.get_state()["status"] & ~16) == 0)
 
 
 if __name__ == "__main__":
