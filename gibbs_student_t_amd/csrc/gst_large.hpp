@@ -1401,7 +1401,69 @@ __global__ void __launch_bounds__(TB) lg_toa(const DevModel* __restrict__ mds, L
       theta = ga / (ga + gb);
     }
   }
-  if ((a.mask & 16u) && mix) {
+  const bool fuse = (a.mask & 16u) && mix && (a.mask & 32u) && md.vary_alpha;
+  const bool fuse_nu = fuse && (a.mask & 64u) && md.vary_df;
+  double zs_new = 0.0, sa_new = 0.0;
+  LogProd lp_new;
+  if (fuse) {
+    // z, alpha and nu's sums in one pass over the TOAs (each thread its own TOAs, in the
+    // separate passes' order): alpha is drawn from the new z right away and kept if the new z
+    // has an outlier (gibbs.py:234; the old alpha waits in the w scratch row otherwise), so
+    // alpha / nu cost no extra passes over z, y, alpha.  Draws and sums are bitwise the
+    // separate passes'.
+    const double SQ2PI = 2.5066282746310002;  // np.sqrt(2*np.pi)
+    double* wc = a.s.w + (size_t)c * a.ys;
+    for (int t = tid; t < n; t += TB) {
+      const double N0 = wn.n0(t);
+      const double al_old = alc[t];
+      const double Nv = al_old * N0;
+      const double y = yc[t];
+      const double sd1 = sqrt(Nv);
+      const double x1 = y / sd1;
+      double top = theta * (exp(-(x1 * x1) / 2.0) / SQ2PI / sd1);
+      if (md.model == 3) top = theta / md.pspin;
+      const double sd0 = sqrt(N0);
+      const double x0 = y / sd0;
+      const double bot = top + (1.0 - theta) * (exp(-(x0 * x0) / 2.0) / SQ2PI / sd0);
+      double qz = top / bot;
+      if (isnan(qz)) qz = 1.0;
+      poc[t] = qz;
+      const double pz = qz < 1.0 ? qz : 1.0;
+      double u;
+      if (tp) {
+        u = tp[TP_DELTA + m + 1 + t];
+      } else {
+        double unused;
+        rng.uniform2((uint32_t)t, TAG_Z, u, unused);
+      }
+      const double zf = (double)bern_legacy(pz, u);
+      zc[t] = zf;
+      const double atop = ((y * y) * zf / N0 + nu) / 2.0;
+      const double G = tp ? tp[TP_DELTA + m + 1 + nst + t]
+                          : gamma_mt((zf + nu) / 2.0, rng, (uint32_t)t, TAG_ALPHA);
+      const double an = atop / G;
+      wc[t] = al_old;
+      alc[t] = an;
+      zs_new += zf;
+      if (fuse_nu) {
+        lp_new.mul(an);
+        sa_new += 1.0 / an;
+      }
+    }
+    zs_new = block_sum<TB / 64>(zs_new, red);
+    if (!(zs_new >= 1.0)) {
+      // no outlier flagged: alpha keeps its values (gibbs.py:234,242), nu sums over them
+      lp_new = LogProd();
+      sa_new = 0.0;
+      for (int t = tid; t < n; t += TB) {
+        const double ao = wc[t];
+        alc[t] = ao;
+        lp_new.mul(ao);
+        sa_new += 1.0 / ao;
+      }
+    }
+  }
+  if ((a.mask & 16u) && mix && !fuse) {
     const double SQ2PI = 2.5066282746310002;  // np.sqrt(2*np.pi)
     for (int t = tid; t < n; t += TB) {
       const double N0 = wn.n0(t);
@@ -1429,7 +1491,7 @@ __global__ void __launch_bounds__(TB) lg_toa(const DevModel* __restrict__ mds, L
     }
   }
   __syncthreads();
-  if ((a.mask & 32u) && md.vary_alpha) {
+  if ((a.mask & 32u) && md.vary_alpha && !fuse) {
     double zs = 0.0;
     for (int t = tid; t < n; t += TB) zs += (zc[t] != 0.0) ? 1.0 : 0.0;
     zs = block_sum<TB / 64>(zs, red);
@@ -1446,11 +1508,13 @@ __global__ void __launch_bounds__(TB) lg_toa(const DevModel* __restrict__ mds, L
   }
   __syncthreads();
   if ((a.mask & 64u) && md.vary_df) {
-    double sa = 0.0;
-    LogProd lp;
-    for (int t = tid; t < n; t += TB) {
-      lp.mul(alc[t]);
-      sa += 1.0 / alc[t];
+    double sa = sa_new;
+    LogProd lp = lp_new;
+    if (!fuse_nu) {
+      for (int t = tid; t < n; t += TB) {
+        lp.mul(alc[t]);
+        sa += 1.0 / alc[t];
+      }
     }
     const double S = block_sum<TB / 64>(lp.log_sum() + sa, red);
     if (tid < 64) {
