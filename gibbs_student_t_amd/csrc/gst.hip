@@ -609,7 +609,7 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
   const dim3 g_gs((C + gst::GS_WPB - 1) / gst::GS_WPB), b_gs(64 * gst::GS_WPB);
   const dim3 g_chain(C), b_chain(gst::LBLK), b_toa(small_toa ? gst::TBLK_SMALL : gst::TBLK);
   const dim3 g_gram(npairs * ((C + gst::GRAM_WAVES - 1) / gst::GRAM_WAVES)), b_gram(64 * gst::GRAM_WAVES);
-  const dim3 g_tb(ys / 64, (C + 63) / 64);
+  const dim3 g_tb(ys / 64, (C + 64 * gst::TB_CG - 1) / (64 * gst::TB_CG));
   cx->evused = 0;
   HIP_OK(hipEventRecord(cx->ev0, st));
   LG_LAUNCH(GST_K_TB, gst::lg_tb, g_tb, b_chain, 0);   // y = r - T b for the current b

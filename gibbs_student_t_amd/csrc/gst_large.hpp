@@ -47,6 +47,7 @@ constexpr int TBLK_WAVE = 64;
 constexpr int TBLK_WAVE_NPAD = 8192;
 constexpr int GRAM_WAVES = 8;  // chains per gram workgroup
 constexpr int TM_PW = 16;      // panel width of the timing-model elimination
+constexpr int TM_TILES = 4;   // trailing-update tiles per wave per round (lg_tmelim)
 
 struct LScratch {
   double* G;   // [C][mp*mp] Gram (row-major, lower triangle); kept for the floor pass
@@ -739,23 +740,42 @@ __global__ void __launch_bounds__(LBLK) lg_tmelim(const DevModel* __restrict__ m
     const int k1 = k0 + TM_PW;
     const int TR = (mp - k1) / 16;
     const int ntile = TR * (TR + 1) / 2;
-    for (int e = wv; e < ntile; e += LBLK / 64) {
-      int X = 0;
-      while ((X + 1) * (X + 2) / 2 <= e) ++X;
-      const int Y = e - X * (X + 1) / 2;
-      const int r0 = k1 + 16 * X, c0 = k1 + 16 * Y;
-      v4d acc;
+    // TM_TILES tiles per wave per round, their loads issued first (the rounds were bound by
+    // one global load round trip per tile); tiles past ntile in the last round are masked
+    constexpr int NW = LBLK / 64;
+    for (int e0 = wv; e0 < ntile; e0 += TM_TILES * NW) {
+      int r0[TM_TILES], c0[TM_TILES];
+      bool in[TM_TILES];
+      v4d acc[TM_TILES];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) acc[g] = Gin[(size_t)(r0 + (lane >> 4) + 4 * g) * mp + c0 + (lane & 15)];
+      for (int h = 0; h < TM_TILES; ++h) {
+        const int e = e0 + h * NW;
+        in[h] = e < ntile;
+        const int ee = in[h] ? e : e0;
+        int X = 0;
+        while ((X + 1) * (X + 2) / 2 <= ee) ++X;
+        const int Y = ee - X * (X + 1) / 2;
+        r0[h] = k1 + 16 * X;
+        c0[h] = k1 + 16 * Y;
 #pragma unroll
-      for (int k4 = 0; k4 < TM_PW / 4; ++k4) {
-        const int kk = 4 * k4 + (lane >> 4);
-        const double av = -P[(r0 - k0 + (lane & 15)) * PS + kk];
-        const double bv = P[(c0 - k0 + (lane & 15)) * PS + kk] * ainv[kk];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        for (int g = 0; g < 4; ++g)
+          acc[h][g] = Gin[(size_t)(r0[h] + (lane >> 4) + 4 * g) * mp + c0[h] + (lane & 15)];
       }
 #pragma unroll
-      for (int g = 0; g < 4; ++g) Gc[(size_t)(r0 + (lane >> 4) + 4 * g) * mp + c0 + (lane & 15)] = acc[g];
+      for (int h = 0; h < TM_TILES; ++h) {
+#pragma unroll
+        for (int k4 = 0; k4 < TM_PW / 4; ++k4) {
+          const int kk = 4 * k4 + (lane >> 4);
+          const double av = -P[(r0[h] - k0 + (lane & 15)) * PS + kk];
+          const double bv = P[(c0[h] - k0 + (lane & 15)) * PS + kk] * ainv[kk];
+          acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[h], 0, 0, 0);
+        }
+        if (in[h]) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            Gc[(size_t)(r0[h] + (lane >> 4) + 4 * g) * mp + c0[h] + (lane & 15)] = acc[h][g];
+        }
+      }
     }
     __syncthreads();
   }
@@ -1326,44 +1346,96 @@ __global__ void __launch_bounds__(LBLK) lg_btm(const DevModel* __restrict__ mds,
 // ------------------------------------------------------------------------------------
 // tb: y = r - T b for every chain (gibbs.py:213,237,272) as one MFMA GEMM
 // ------------------------------------------------------------------------------------
-// Wave: 16 chains x 64 TOAs (4 tiles); A = b (chains x basis), B = T^T (basis x TOAs) read
-// from the column-major Tcol so a wave's B fragment is 16 consecutive TOAs.
-__global__ void __launch_bounds__(LBLK) lg_tb(const DevModel* __restrict__ mds, LArgs a) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int t0 = blockIdx.x * 64;
-  const int cb = (blockIdx.y * 4 + wv) * 16;
-  if (cb >= a.C) return;
-  const DevModel& md = mds[ds_of(a, cb)];         // one dataset per 16-chain group
+// Wave: CG groups of 16 chains x 64 TOAs (4 tiles); A = b (chains x basis), B = T^T (basis x
+// TOAs) read from the column-major Tcol so a wave's B fragment is 16 consecutive TOAs.  The
+// groups of a wave share the B fragments (CG x 4 MFMAs per CG + 4 loads), with TB_DEPTH
+// k-steps of operands in flight.  Every y element receives the same MFMA sequence (k in
+// order, the same A / B values) whatever CG is, so y is bitwise that of one group per wave.
+constexpr int TB_CG = 4;      // 16-chain groups per wave (chains per wave: 64)
+constexpr int TB_DEPTH = 2;   // k-steps of operands in flight
+template <int CG>
+__device__ __forceinline__ void tb_tile(const DevModel& md, const LArgs& a, int t0, int cb) {
+  const int lane = threadIdx.x & 63;
   const int m = md.m, npad = md.npad;
   if (t0 >= npad) return;                         // beyond this dataset's TOAs
-  const int ci = cb + (lane & 15);
-  const bool cok = ci < a.C;
-  const double* bc = a.st.b + (size_t)(cok ? ci : cb) * m;
-  v4d acc[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) acc[u] = (v4d){0.0, 0.0, 0.0, 0.0};
   const int kl = lane >> 4;
-#pragma unroll 2
-  for (int k = 0; k < m; k += 4) {
+  const double* bc[CG];
+  bool cok[CG];
+#pragma unroll
+  for (int g = 0; g < CG; ++g) {
+    const int ci = cb + 16 * g + (lane & 15);
+    cok[g] = ci < a.C;
+    bc[g] = a.st.b + (size_t)(cok[g] ? ci : cb) * m;
+  }
+  v4d acc[CG][4];
+#pragma unroll
+  for (int g = 0; g < CG; ++g)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[g][u] = (v4d){0.0, 0.0, 0.0, 0.0};
+  constexpr int D = TB_DEPTH;
+  double av[D][CG], bv[D][4];
+  auto load = [&](int d, int k) __attribute__((always_inline)) {
     const int j = k + kl;
     const bool jok = j < m;
-    const double av = (cok && jok) ? bc[j] : 0.0;
     const double* tc = md.Tcol + (size_t)(jok ? j : 0) * npad + t0 + (lane & 15);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const double bv = jok ? tc[16 * u] : 0.0;
-      acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[u], 0, 0, 0);
+    for (int g = 0; g < CG; ++g) av[d][g] = (cok[g] && jok) ? bc[g][jok ? j : 0] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) bv[d][u] = jok ? tc[16 * u] : 0.0;
+  };
+  auto kstep = [&](int d) __attribute__((always_inline)) {
+#pragma unroll
+    for (int g = 0; g < CG; ++g)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        acc[g][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[d][g], bv[d][u], acc[g][u], 0, 0, 0);
+  };
+  const int nks = (m + 3) / 4;                    // k-steps (the last one zero-padded)
+#pragma unroll
+  for (int d = 0; d < D; ++d) load(d, 4 * d);
+  int ks = 0;
+  for (; ks + D < nks; ks += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      kstep(d);
+      load(d, 4 * (ks + d + D));
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 #pragma unroll
-  for (int u = 0; u < 4; ++u)
+  for (int d = 0; d < D; ++d)
+    if (ks + d < nks) kstep(d);
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int cc = cb + kl + 4 * g;
-      const int t = t0 + 16 * u + (lane & 15);
-      if (cc < a.C && t < npad)
-        a.s.y[(size_t)cc * a.ys + t] = (t < md.n) ? md.resid[t] - acc[u][g] : 0.0;
-    }
+  for (int g = 0; g < CG; ++g)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int cc = cb + 16 * g + kl + 4 * q;
+        const int t = t0 + 16 * u + (lane & 15);
+        if (cc < a.C && t < npad)
+          a.s.y[(size_t)cc * a.ys + t] = (t < md.n) ? md.resid[t] - acc[g][u][q] : 0.0;
+      }
+}
+
+__global__ void __launch_bounds__(LBLK) lg_tb(const DevModel* __restrict__ mds, LArgs a) {
+  const int wv = threadIdx.x >> 6;
+  const int t0 = blockIdx.x * 64;
+  const int cw = (blockIdx.y * 4 + wv) * 16 * TB_CG;   // the wave's first chain
+  if (cw >= a.C) return;
+  // one dataset per 16-chain group (native.py checks it); the groups share T's fragments
+  // when they share the dataset, otherwise each group runs on its own
+  const int d0 = ds_of(a, cw);
+  bool same = true;
+#pragma unroll
+  for (int g = 1; g < TB_CG; ++g)
+    if (cw + 16 * g < a.C && ds_of(a, cw + 16 * g) != d0) same = false;
+  if (same) {
+    tb_tile<TB_CG>(mds[d0], a, t0, cw);
+  } else {
+    for (int g = 0; g < TB_CG; ++g)
+      if (cw + 16 * g < a.C) tb_tile<1>(mds[ds_of(a, cw + 16 * g)], a, t0, cw + 16 * g);
+  }
 }
 
 // ------------------------------------------------------------------------------------

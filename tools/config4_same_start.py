@@ -4,8 +4,9 @@
     python tools/config4_same_start.py compare D GPU.npz ORACLE_SVD.npz [ORACLE_FLOOR.npz] OUT.json
 
 ``oracle``: the reference algorithm (oracle/gibbs_oracle.py with gibbs.py's legacy RNG calls)
-on dataset D of bench.py's config-4 grid, 64 chains from EXACTLY the GPU chains' initial
-states (run_sims.initial_state(entry, 64, 64 D, 7, ...): the prior draws and gibbs.py:29-51
+on dataset D of bench.py's config-4 grid, NCHAINS (64) chains from EXACTLY the initial states
+of the GPU chains of ``config4_rhat.py --chains NCHAINS`` (run_sims.initial_state(entry,
+NCHAINS, NCHAINS D, 7, ...): the prior draws and gibbs.py:29-51
 latents bench.workload gives them, vvh17 at the reference's z = 1), on the bench schedule
 (4300 sweeps, then a 5000-sweep window recorded every 5th sweep).  VARIANT ``svd`` is the
 reference's own b draw (gibbs.py:169-180); ``floor`` the HIP path's rule (exact draw, at the
@@ -46,7 +47,8 @@ def _chain(args):
     from oracle.gibbs_oracle import ChainState, LegacyNumpyVariates, Oracle, OutlierModel
     e = _entry(d)
     n = e.pta.n
-    init = run_sims.initial_state(e, nch, d * CHAINS, SEED0, n, "reference")
+    # bench.workload(4, chains=nch) gives dataset d the chain ids d*nch .. d*nch + nch - 1
+    init = run_sims.initial_state(e, nch, d * nch, SEED0, n, "reference")
     orc = Oracle(e.pta, OutlierModel(**e.cfg))
     st = ChainState(b=init["b"][c].copy(), z=init["z"][c, :n].copy(),
                     alpha=init["alpha"][c, :n].copy(), pout=init["pout"][c, :n].copy(),
@@ -64,7 +66,7 @@ def _chain(args):
 
 
 def run_oracle(d, variant, out, nch=CHAINS):
-    """Chains 0..63 start exactly as the GPU's; NCHAINS > 64 adds further prior draws."""
+    """NCHAINS chains starting exactly as the GPU's config4_rhat.py --chains NCHAINS."""
     with Pool(8) as pool:
         res = pool.map(_chain, [(d, variant, c, nch) for c in range(nch)], chunksize=1)
     e = _entry(d)
