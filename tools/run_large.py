@@ -2,6 +2,7 @@
 
     python tools/run_large.py [sweeps] [chains] [n] [components] [ntm] [warmup sweeps]
 """
+import os
 import sys
 import time
 
@@ -10,7 +11,7 @@ import torch
 
 sys.path.insert(0, ".")
 from bench import CFG, initial_state  # noqa: E402
-from gibbs_student_t_amd import data  # noqa: E402
+from gibbs_student_t_amd import _abi, data  # noqa: E402
 from gibbs_student_t_amd.model import PTA  # noqa: E402
 from gibbs_student_t_amd.native import NativeSampler  # noqa: E402
 
@@ -31,7 +32,9 @@ def main():
         ns.synchronize()
     ns.set_timing(True)
     t0 = time.perf_counter()
-    ns.sweep(S, seed=1, sweep0=W)
+    # RL_MASK: stage mask of the timed sweeps (include/gst.h), e.g. without the white MH
+    mask = int(os.environ.get("RL_MASK", "0"), 0) or _abi.STAGE_ALL
+    ns.sweep(S, seed=1, sweep0=W, mask=mask)
     ns.synchronize()
     dt = time.perf_counter() - t0
     kt = ns.kernel_times()
