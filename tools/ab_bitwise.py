@@ -6,6 +6,8 @@ semantics-neutral, e.g. the paired elimination tail, must leave every draw uncha
 Each library runs in its own process (GST_LIB) from the same prior-draw start, on the
 J1713+0747 headline workload and on the config-3 / 20-component / 22-TM-column fixtures'
 datasets, recording every sweep; the records and final states are compared bitwise.
+AB_CASES picks the cases (also syn<N>k: a scaled synthetic pulsar of N thousand TOAs), AB_PATH
+the sampler path (auto / persistent / large).
 """
 import os
 import subprocess
@@ -25,15 +27,23 @@ def worker(case, C, S, out):
     from golden_io import load_dataset
     from gibbs_student_t_amd.native import NativeSampler
     cfg = dict(model="mixture", vary_df=True, theta_prior="beta")
-    pta = load_dataset(dataset=case) if case != "j1713" else load_dataset()
-    ns = NativeSampler(pta, cfg, 0)
+    if case.startswith("syn"):        # scaled synthetic pulsar, n = syn<N>k TOAs (large path)
+        from gibbs_student_t_amd import data
+        from gibbs_student_t_amd.model import PTA
+        n = int(case[3:].rstrip("k")) * 1000
+        pta = PTA(data.scaled_synthetic(n=n, components=30, ntm=50, seed=5), components=30)
+    else:
+        pta = load_dataset(dataset=case) if case != "j1713" else load_dataset()
+    ns = NativeSampler(pta, cfg, 0, path=os.environ.get("AB_PATH", "auto"))
     ns.alloc(C)
     lo = np.array([p.pmin for p in pta.params])
     hi = np.array([p.pmax for p in pta.params])
     ns.set_state(x=np.random.default_rng(3).uniform(lo, hi, size=(C, len(lo))),
                  z=np.ones((C, ns.n)), alpha=np.ones((C, ns.n)), theta=np.full(C, 0.01),
                  nu=np.full(C, 4.0))
-    rec = ns.alloc_records(S)
+    # per-TOA records only for small pulsars (C x S x n doubles each)
+    rec = ns.alloc_records(S, keys=("x", "b", "theta", "nu")) if ns.n > 4096 else \
+        ns.alloc_records(S)
     ns.sweep(S, records=rec, seed=99)
     fin = ns.get_state()
     np.savez(out, **{f"rec_{k}": v.cpu().numpy() for k, v in rec.items()},
