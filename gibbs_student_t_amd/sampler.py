@@ -60,6 +60,8 @@ class Gibbs:
         self._tdf_all = np.full(C, float(tdf))
         cfg = dict(model=model, tdf=tdf, m=m, vary_df=vary_df, theta_prior=theta_prior,
                    vary_alpha=vary_alpha, alpha=alpha, pspin=pspin)
+        self._cfg = dict(cfg, exact_bdraw=bool(exact_bdraw))
+        self._x_all = None
         self._native = NativeSampler(pta, cfg, device)
         self._native.set_debug(exact_bdraw=exact_bdraw)
         self._native.alloc(C)
@@ -132,6 +134,7 @@ class Gibbs:
         s = self._native.get_state()
         self._b_all, self._z_all, self._alpha_all = s["b"], s["z"], s["alpha"]
         self._pout_all, self._theta_all, self._tdf_all = s["pout"], s["theta"], s["nu"]
+        self._x_all = s["x"]
         self.status = s["status"]
         return s["x"]
 
@@ -234,5 +237,75 @@ class Gibbs:
         x = self._pull()
         return x[0] if C == 1 else x
 
+    # ---- checkpoint / resume (not in the reference: gibbs.py:344-350 restarts its chains) --
+    def checkpoint(self):
+        """The sampler's whole state after ``sample``: every chain's x and latents (b, z,
+        alpha, pout, theta, nu), the Philox key and sweep counter, the model options and the
+        basis shape.  A sampler restored from it continues the chains bitwise: the kernels
+        keep no state across launches, and the variates of a sweep are keyed
+        by (seed, sweep index, chain)."""
+        if self._x_all is None:
+            raise RuntimeError("checkpoint() needs a finished sample() call")
+        return make_checkpoint(self._cfg, self.pta.get_basis()[0].shape, self.seed,
+                               self._sweep_counter, x=self._x_all, b=self._b_all,
+                               z=self._z_all, alpha=self._alpha_all, pout=self._pout_all,
+                               theta=self._theta_all, nu=self._tdf_all)
+
+    def save_checkpoint(self, path):
+        """``checkpoint()`` as an .npz file (plain arrays, no pickles)."""
+        np.savez(path, **self.checkpoint())
+
+    def load_checkpoint(self, ckpt):
+        """Restore a ``checkpoint()`` (dict or .npz path) into this sampler, which must have
+        the same model options, basis shape and chain count; returns x to pass to
+        ``sample`` (the chains then continue where the checkpointed ones stopped)."""
+        if not isinstance(ckpt, dict):
+            with np.load(ckpt, allow_pickle=False) as f:
+                ckpt = {k: f[k] for k in f.files}
+        check_checkpoint(ckpt, self._cfg, self.pta.get_basis()[0].shape, self.nchains)
+        self.seed = int(ckpt["seed"])
+        self._sweep_counter = int(ckpt["sweep_counter"])
+        self._b_all = np.array(ckpt["b"], dtype=np.float64)
+        self._z_all = np.array(ckpt["z"], dtype=np.float64)
+        self._alpha_all = np.array(ckpt["alpha"], dtype=np.float64)
+        self._pout_all = np.array(ckpt["pout"], dtype=np.float64)
+        self._theta_all = np.array(ckpt["theta"], dtype=np.float64)
+        self._tdf_all = np.array(ckpt["nu"], dtype=np.float64)
+        self._x_all = np.array(ckpt["x"], dtype=np.float64)
+        return self._x_all[0] if self.nchains == 1 else self._x_all
+
     def close(self):
         self._native.close()
+
+
+CKPT_VERSION = 1
+_CKPT_OPTS = ("model", "tdf", "m", "vary_df", "theta_prior", "vary_alpha", "alpha", "pspin",
+              "exact_bdraw")
+
+
+def make_checkpoint(cfg, basis_shape, seed, sweep_counter, **state):
+    """Checkpoint dict: state arrays (leading chain axis) + key, counter, options, shape."""
+    ck = {k: np.asarray(v, dtype=np.float64) for k, v in state.items()}
+    ck.update(version=np.int64(CKPT_VERSION), seed=np.uint64(seed),
+              sweep_counter=np.int64(sweep_counter), n=np.int64(basis_shape[0]),
+              m=np.int64(basis_shape[1]),
+              options=np.array([f"{k}={cfg.get(k)!r}" for k in _CKPT_OPTS]))
+    return ck
+
+
+def check_checkpoint(ck, cfg, basis_shape, nchains):
+    """Raise ValueError unless ``ck`` fits a sampler with these options / shape / chains."""
+    if int(ck.get("version", -1)) != CKPT_VERSION:
+        raise ValueError(f"checkpoint version {ck.get('version')} != {CKPT_VERSION}")
+    want = [f"{k}={cfg.get(k)!r}" for k in _CKPT_OPTS]
+    got = [str(v) for v in np.asarray(ck["options"]).tolist()]
+    if got != want:
+        diff = [(a, b) for a, b in zip(got, want) if a != b]
+        raise ValueError(f"checkpoint model options differ: {diff}")
+    if (int(ck["n"]), int(ck["m"])) != tuple(basis_shape):
+        raise ValueError(f"checkpoint basis {int(ck['n'])}x{int(ck['m'])} != "
+                         f"{basis_shape[0]}x{basis_shape[1]}")
+    for k in ("x", "b", "z", "alpha", "pout", "theta", "nu"):
+        if np.asarray(ck[k]).shape[0] != nchains:
+            raise ValueError(f"checkpoint has {np.asarray(ck[k]).shape[0]} chains, "
+                             f"sampler {nchains}")

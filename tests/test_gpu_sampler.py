@@ -157,3 +157,27 @@ def test_batched_chains_and_thinning():
     np.testing.assert_array_equal(g.chain[:, 0], np.tile(ref["xs"], (C, 1)))
     assert np.std(g.chain[:, -1, 0]) > 0                      # chains are independent
     g.close()
+
+
+@pytest.mark.parametrize("name", ["beta_fixed", "vvh17_fixed"])
+def test_checkpoint_resume_is_bitwise(name, tmp_path):
+    """sample(N) -> save_checkpoint -> a NEW sampler -> load_checkpoint -> sample(M) gives
+    the chains of one sample(N + M) run, bitwise (chain arrays, final state)."""
+    ref = load_ref(name)
+    N, M, C = 30, 20, 4
+    g = Gibbs(ref["pta"], **ref["kw"], nchains=C, seed=4242, chunk=16)
+    xa = g.sample(ref["xs"], niter=N + M)
+    full = {k: getattr(g, k).copy() for k in ("chain", "bchain", "zchain", "alphachain",
+                                               "poutchain", "thetachain", "dfchain")}
+    g.close()
+    h = Gibbs(ref["pta"], **ref["kw"], nchains=C, seed=4242, chunk=16)
+    h.sample(ref["xs"], niter=N)
+    h.save_checkpoint(tmp_path / "ck.npz")
+    h.close()
+    r = Gibbs(ref["pta"], **ref["kw"], nchains=C, seed=1)     # key comes from the file
+    x = r.load_checkpoint(tmp_path / "ck.npz")
+    xb = r.sample(x, niter=M)
+    for k, v in full.items():
+        np.testing.assert_array_equal(getattr(r, k), v[:, N:], err_msg=k)
+    np.testing.assert_array_equal(xb, xa)
+    r.close()
