@@ -965,6 +965,10 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   __shared__ double xchg[PAIR ? 2 : 1][2][2];  // pair mode: [round parity][wave] {lnL, failed}
   __shared__ int xdrew[PAIR ? 1 : 1];          // pair mode: the b draw happened this sweep
   __shared__ double xfloor[1];                 // pair mode: the owner's floor_shift
+  // pair mode: z / pout and alpha of the TOA slots the other wave drew (slot s belongs to
+  // wave s & 1), exchanged after each stage
+  __shared__ double xpo[PAIR ? NS : 1][PAIR ? 64 : 1], xal[PAIR ? NS : 1][PAIR ? 64 : 1];
+  __shared__ unsigned long long xzm[PAIR ? NS : 1];
 
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2130,11 +2134,15 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     }
     fair_prio<OCC>(fair);
     // ---- z (gibbs.py:201-226)
+    // pair mode: each wave draws z and alpha for its half of the TOA slots (Philox is keyed
+    // by TOA, so every draw is the one the single-wave kernel makes) and takes the other
+    // half from its partner through LDS
+    const unsigned mine = PAIR ? (vmask & (role ? 0xAAAAAAAAu : 0x55555555u)) : vmask;
     if ((mask & 16u) && mix) {
       const double SQ2PI = 2.5066282746310002;  // np.sqrt(2*np.pi)
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        if (vmask & (1u << s)) {
+        if (mine & (1u << s)) {
           const int t = 64 * s + lane;
           const double N0 = ef2 * S2(s) + Q;
           const double Nv = al[s] * N0;
@@ -2161,6 +2169,24 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
           zb = (zb & ~(1u << s)) | ((unsigned)zz << s);
         }
       }
+      if constexpr (PAIR) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          const unsigned long long bm = __ballot((zb >> s) & 1u);
+          if ((s & 1) == role) {
+            xpo[s][lane] = po[s];
+            if (lane == 0) xzm[s] = bm;
+          }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          if ((s & 1) != role) {
+            po[s] = xpo[s][lane];
+            zb = (zb & ~(1u << s)) | ((unsigned)((xzm[s] >> lane) & 1ull) << s);
+          }
+        }
+      }
     }
     fair_prio<OCC>(fair);
     // ---- alpha (gibbs.py:229-242)
@@ -2180,16 +2206,25 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
           double sh[NS];
 #pragma unroll
           for (int s = 0; s < NS; ++s) sh[s] = ((double)((zb >> s) & 1u) + nu) / 2.0;
-          gamma_mt_slots<NS>(sh, vmask, rng, (uint32_t)lane, TAG_ALPHA, G);
+          gamma_mt_slots<NS>(sh, mine, rng, (uint32_t)lane, TAG_ALPHA, G);
         }
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-          if (vmask & (1u << s)) {
+          if (mine & (1u << s)) {
             const double zf = (double)((zb >> s) & 1u);
             const double N0 = ef2 * S2(s) + Q;
             const double top = ((yv[s] * yv[s]) * zf / N0 + nu) / 2.0;
             al[s] = top / G[s];
           }
+        }
+        if constexpr (PAIR) {
+#pragma unroll
+          for (int s = 0; s < NS; ++s)
+            if ((s & 1) == role) xal[s][lane] = al[s];
+          __syncthreads();
+#pragma unroll
+          for (int s = 0; s < NS; ++s)
+            if ((s & 1) != role) al[s] = xal[s][lane];
         }
       }
     }
