@@ -968,6 +968,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   // pair mode: z / pout and alpha of the TOA slots the other wave drew (slot s belongs to
   // wave s & 1), exchanged after each stage
   __shared__ double xpo[PAIR ? NS : 1][PAIR ? 64 : 1], xal[PAIR ? NS : 1][PAIR ? 64 : 1];
+  __shared__ double xyv[PAIR ? NS : 1][PAIR ? 64 : 1];   // pair mode: the drawer's y = r - T b
   __shared__ unsigned long long xzm[PAIR ? NS : 1];
 
   const int lane = threadIdx.x & 63;
@@ -2102,12 +2103,25 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         if (drew) {
           double* pb = smem[role ^ 1] + (bsc - smem[role]);
           for (int j = lane; j < m; j += 64) pb[j] = bsc[j];
+          // and its y = r - T b (compute_Tb's values: the partner copies them instead of
+          // repeating the T b product)
+          if (owner >= 0) {
+#pragma unroll
+            for (int s = 0; s < NS; ++s) xyv[s][lane] = yv[s];
+          }
         }
         if (role == (owner >= 0 ? owner : 0) && lane == 0) xdrew[0] = drew ? 1 : 0;
         __syncthreads();
         const bool got = xdrew[0] != 0;
-        __syncthreads();   // xdrew is rewritten next sweep
-        if (got && role != owner) compute_Tb();
+        if (got && role != owner) {
+          if (owner >= 0) {
+#pragma unroll
+            for (int s = 0; s < NS; ++s) yv[s] = xyv[s][lane];
+          } else {
+            compute_Tb();
+          }
+        }
+        __syncthreads();   // xdrew and xyv are rewritten next sweep
       }
     }
 
