@@ -10,7 +10,10 @@ grep -E "identical|DIFFER" $O/bitwise.log
 for r in 1 2 3; do
   for lib in gibbs_student_t_amd/libgst_ab_head.so gibbs_student_t_amd/libgst.so; do
     n=$(basename $lib .so)
-    GST_LIB=$lib timeout -k 10 120 python -u bench.py --no-cpu-baseline --ess-window 0 --no-stage-costs --config 3 --steps 500 --warmup 50 > $O/$n.$r.json 2> $O/$n.$r.err || { echo FAIL; tail -3 $O/$n.$r.err; exit 1; }
-    python -c "import json;d=json.load(open('$O/$n.$r.json'));print('$n r$r %10.0f kernel %.4f ms/sweep'%(d['value'],d['kernel_ms']/d['steps']))"
+    for a in "--config 3" "--chains 512"; do
+      tag=$(echo "$a" | tr -d ' -')
+      GST_LIB=$lib timeout -k 10 120 python -u bench.py --no-cpu-baseline --ess-window 0 --no-stage-costs $a --steps 500 --warmup 50 > $O/$n.$tag.$r.json 2> $O/$n.$tag.$r.err || { echo FAIL; tail -3 $O/$n.$tag.$r.err; exit 1; }
+      python -c "import json;d=json.load(open('$O/$n.$tag.$r.json'));print('$n $tag r$r %10.0f kernel %.4f ms/sweep'%(d['value'],d['kernel_ms']/d['steps']))"
+    done
   done
 done
