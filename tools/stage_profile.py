@@ -1,6 +1,7 @@
 """Per-stage cycle breakdown of the sweep kernel (diagnostic libgst_stamps.so).
 
 Usage: GST_LIB=gibbs_student_t_amd/libgst_stamps.so python tools/stage_profile.py [C] [S] [waves]
+(SP_CONFIG=3: bench config 3's pulsar instead of J1713+0747)
 Stamps fence the overlaps of the real kernel: read the SHARES, not the absolute length.
 """
 import ctypes as ct
@@ -25,15 +26,23 @@ def main():
     C = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
     S = int(sys.argv[2]) if len(sys.argv) > 2 else 50
     waves = int(sys.argv[3]) if len(sys.argv) > 3 else "auto"
-    pta = PTA(data.j1713())
-    ns = NativeSampler(pta, dict(model="mixture", vary_df=True, theta_prior="beta"), 0)
-    ns.set_waves(waves)
-    ns.alloc(C)
-    rng = np.random.default_rng(0)
-    x0 = np.stack([[rng.uniform(1, 7), rng.uniform(-18, -12), rng.uniform(-10, -5)]
-                   for _ in range(C)])
-    ns.set_state(x=x0, z=np.ones((C, ns.n)), alpha=np.ones((C, ns.n)),
-                 theta=np.full(C, 0.01), nu=np.full(C, 4.0))
+    if os.environ.get("SP_CONFIG") == "3":   # bench config 3's pulsar (130 distinct sigmas)
+        import bench
+        wl = bench.workload(3, 0, 1, C)
+        ns = NativeSampler(wl["ptas"], wl["cfgs"], 0)
+        ns.set_waves(waves)
+        ns.alloc(C)
+        ns.set_state(**wl["init"])
+    else:
+        pta = PTA(data.j1713())
+        ns = NativeSampler(pta, dict(model="mixture", vary_df=True, theta_prior="beta"), 0)
+        ns.set_waves(waves)
+        ns.alloc(C)
+        rng = np.random.default_rng(0)
+        x0 = np.stack([[rng.uniform(1, 7), rng.uniform(-18, -12), rng.uniform(-10, -5)]
+                       for _ in range(C)])
+        ns.set_state(x=x0, z=np.ones((C, ns.n)), alpha=np.ones((C, ns.n)),
+                     theta=np.full(C, 0.01), nu=np.full(C, 4.0))
     ns.sweep(300, seed=1)
     buf = torch.zeros((C, 24), dtype=torch.int64, device=ns.tdev)
     _abi.check(ns.lib, ns.lib.gst_debug_stamps(ns.ctx, ct.c_void_p(buf.data_ptr())),
