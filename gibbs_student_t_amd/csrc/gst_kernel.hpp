@@ -1098,16 +1098,37 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
 
   // sum of log-priors (gibbs.py:337-339): every prior is uniform, so the sum is the
   // host-evaluated constant (Python sum order) when all parameters are in bounds, else -inf
+  // one-wave-per-SIMD builds (registers to spare): the prior bounds and efac choice held in
+  // registers for the launch instead of re-read from the model descriptor at every call
+  // (no machine LICM in this build: each read was a load and a wait)
+  double hpmin[4], hpmax[4], hlp = 0.0, hefc = 1.0;
+  int hief = -1;
+  if constexpr (OCC == 1) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      hpmin[j] = j < P ? md.pmin[j] : 0.0;
+      hpmax[j] = j < P ? md.pmax[j] : 0.0;
+    }
+    hlp = md.lp_sum;
+    hief = md.idx_efac;
+    hefc = md.efac_const;
+  }
   auto lnprior = [&](const double (&xq)[4]) __attribute__((always_inline)) -> double {
     bool in = true;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (j < P) in = in && (xq[j] >= md.pmin[j]) && (xq[j] <= md.pmax[j]);
-    return in ? md.lp_sum : -INFINITY;
+    for (int j = 0; j < 4; ++j) {
+      if (OCC == 1) {
+        if (j < P) in = in && (xq[j] >= hpmin[j]) && (xq[j] <= hpmax[j]);
+      } else {
+        if (j < P) in = in && (xq[j] >= md.pmin[j]) && (xq[j] <= md.pmax[j]);
+      }
+    }
+    return in ? (OCC == 1 ? hlp : md.lp_sum) : -INFINITY;
   };
 
   auto efac2_of = [&](const double (&xq)[4]) __attribute__((always_inline)) -> double {
-    const double ef = md.idx_efac >= 0 ? pget(xq, md.idx_efac) : md.efac_const;
+    const double ef = OCC == 1 ? (hief >= 0 ? pget(xq, hief) : hefc)
+                               : (md.idx_efac >= 0 ? pget(xq, md.idx_efac) : md.efac_const);
     return ef * ef;
   };
 
