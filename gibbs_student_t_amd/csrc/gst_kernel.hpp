@@ -1058,7 +1058,20 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     yv[s] = 0.0;
   }
   auto RR = [&](int s) __attribute__((always_inline)) -> double { return md.resid[64 * s + lane]; };
-  auto S2 = [&](int s) __attribute__((always_inline)) -> double { return md.sig2[64 * s + lane]; };
+  // one-wave-per-SIMD builds: sigma^2 of the lane's TOAs in registers for the launch (the
+  // per-TOA white likelihood reads it 21 times a sweep, each a pointer load, a global load
+  // and a wait without machine LICM); the two-chains-per-SIMD build has no registers to spare
+  double s2r[OCC == 1 ? NS : 1];
+  if constexpr (OCC == 1) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) s2r[s] = ((vmask >> s) & 1u) ? md.sig2[64 * s + lane] : 0.0;
+  }
+  auto S2 = [&](int s) __attribute__((always_inline)) -> double {
+    if constexpr (OCC == 1)
+      return s2r[s];
+    else
+      return md.sig2[64 * s + lane];
+  };
   int status = 0;
   lds_order();
 
