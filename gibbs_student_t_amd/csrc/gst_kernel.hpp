@@ -1511,13 +1511,18 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   const double ldf_l = f_live ? md.ldf[lane] : 0.0;
 
   // b-marginalised likelihood at xq (gibbs.py:288-329); factor left in L.
+  // the descriptor scalars of lnl_hyper, read once for the launch (wave-uniform: scalar
+  // registers), not at each of the ~11 calls per sweep
+  const int hidxA = md.idx_logA, hidxg = md.idx_gamma, hntmp = md.ntm_pad, hnf = md.nf;
+  const double hl12 = md.log_12pi2, hlfyr = md.log_fyr, hslf = md.sum_lfreq,
+               hsldf = md.sum_ldf, hldtm = md.logdet_phi_tm;
   auto lnl_hyper = [&](const double (&xq)[4], int& failed) __attribute__((always_inline)) -> double {
     GST_COUNT(16)
     GST_SUB_BEGIN
-    const double lA = pget(xq, md.idx_logA);
-    const double g = pget(xq, md.idx_gamma);
+    const double lA = pget(xq, hidxA);
+    const double g = pget(xq, hidxg);
     // log phi_k = 2 lA ln10 - log(12 pi^2) + (g-3) log fyr - g log f_k + log df_k
-    const double lc = 2.0 * lA * 2.302585092994045684 - md.log_12pi2 + (g - 3.0) * md.log_fyr;
+    const double lc = 2.0 * lA * 2.302585092994045684 - hl12 + (g - 3.0) * hlfyr;
     // S0 first: its 36 LDS loads are in flight while phi^-1 is computed (exp)
 #pragma unroll
     for (int r = K0; r < MT; ++r)
@@ -1525,14 +1530,13 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       for (int s = K0; s <= r; ++s) L[SL(r, s)] = S0[64 * SL(r - K0, s - K0)];
     // Fourier columns, then the unit-prior dummies that pad a smaller model up to this
     // instance's RA (zero Gram rows: each is eliminated as an exact no-op)
-    if (lane < RA - md.ntm_pad)
-      phbuf[md.ntm_pad + lane] = f_live ? exp(-(lc - g * lfreq_l + ldf_l)) + fshift : 1.0;
+    if (lane < RA - hntmp)
+      phbuf[hntmp + lane] = f_live ? exp(-(lc - g * lfreq_l + ldf_l)) + fshift : 1.0;
     // phbuf doubles as the eliminations' junk rows: restore the one other entry read
     // below, the augmented row's (no prior on the residual column)
     if (lane == 63) phbuf[raug] = 0.0;
     // sum_k log phi_k in closed form (no reduction on the critical path)
-    const double logdet_phi =
-        ((double)md.nf * lc - g * md.sum_lfreq + md.sum_ldf) + md.logdet_phi_tm;
+    const double logdet_phi = ((double)hnf * lc - g * hslf + hsldf) + hldtm;
     lds_order();
 #pragma unroll
     for (int r = K0; r < MT; ++r)
