@@ -1057,7 +1057,17 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     zb |= (zz != 0.0) ? (1u << s) : 0u;
     yv[s] = 0.0;
   }
-  auto RR = [&](int s) __attribute__((always_inline)) -> double { return md.resid[64 * s + lane]; };
+  double rrr[OCC == 1 ? NS : 1];   // one-wave-per-SIMD builds: the lanes' residuals, as s2r
+  if constexpr (OCC == 1) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) rrr[s] = ((vmask >> s) & 1u) ? md.resid[64 * s + lane] : 0.0;
+  }
+  auto RR = [&](int s) __attribute__((always_inline)) -> double {
+    if constexpr (OCC == 1)
+      return rrr[s];
+    else
+      return md.resid[64 * s + lane];
+  };
   // one-wave-per-SIMD builds: sigma^2 of the lane's TOAs in registers for the launch (the
   // per-TOA white likelihood reads it 21 times a sweep, each a pointer load, a global load
   // and a wait without machine LICM); the two-chains-per-SIMD build has no registers to spare
@@ -1150,6 +1160,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   //   sum_t log N_t = sum_t log a_t + sum_u c_u log N0_u,
   //   sum_t y_t^2 / N_t = sum_u W_u / N0_u,   W_u = sum_{t in u} y_t^2 / a_t,
   // where sum log a_t and W_u are fixed for the whole white block (b, alpha, z fixed).
+  const int hncls = md.ncls, hieq = md.idx_equad;   // read once for the launch (scalars)
   double wcls_la = 0.0;   // sum_t log a_t
   auto white_prep = [&]() __attribute__((always_inline)) {
     if (md.ncls == 0) return;
@@ -1176,12 +1187,12 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   // Q = 10^(2 equad) is passed in: the MH steps carry it (Q_q = Q_x * 10^(2 delta)).
   auto lnl_white = [&](const double (&xq)[4], double Q) __attribute__((always_inline)) -> double {
     const double ef2 = efac2_of(xq);
-    if (md.ncls == 1) {  // uniform: no reduction
+    if (hncls == 1) {  // uniform: no reduction
       const double N0 = ef2 * md.csig2[0] + Q;
       return -0.5 * ((wcls_la + md.ccount[0] * log(N0)) + rdlane(wcls, 0) / N0);
     }
     double sl = 0.0, sq = 0.0;
-    if (md.ncls > 1) {
+    if (hncls > 1) {
       if (lane < md.ncls) {
         const double N0 = ef2 * md.csig2[lane] + Q;
         sl = md.ccount[lane] * log(N0);
@@ -1743,7 +1754,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     } else if ((mask & 1u) || eval_only) {
       white_prep();
       double l0 = 0.0, p0 = 0.0;
-      double Qx = exp(2.0 * pget(xv, md.idx_equad) * 2.302585092994045684);
+      double Qx = exp(2.0 * pget(xv, hieq) * 2.302585092994045684);
 #pragma unroll 1
       for (int step = -1; step < NWHITE; ++step) {
         if ((step & 3) == 0) fair_prio<OCC>(fair);
@@ -1755,7 +1766,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
           double E;
           int par;
           luacc = propose(xv, qv, step, E, par);
-          if (par == md.idx_equad) Qq = Qx * E;
+          if (par == hieq) Qq = Qx * E;
         }
         const double p1 = lnprior(qv);
         // out-of-prior: (l1 + -inf) - (l0 + p0) is -inf or NaN, never > log(u): skip lnL
