@@ -1574,7 +1574,8 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     return ll;
   };
 
-  const bool rec_on = record_every > 0 && !eval_only && role == 0;
+  // pair mode: both waves write the records (identical state): b and the TOA slots split
+  const bool rec_on = record_every > 0 && !eval_only && (PAIR || role == 0);
   int hacc = 0, hrej = 0;   // pair mode: hyper-MH acceptance history (branch prediction)
   GST_STAMP_START
   compute_Tb();
@@ -1615,21 +1616,21 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       const int ri = it / record_every;
       if (ri < rec.nrec) {
         const size_t base = (size_t)c * rec.nrec + ri;
-        if (rec.x && lane < P) rec.x[base * P + lane] = pget(xv, lane);
+        if (rec.x && lane < P && role == 0) rec.x[base * P + lane] = pget(xv, lane);
         // from the state row, not bsc: bsc shares S0R with S0 and is stale after a sweep
         // that skipped the b draw (gibbs.py:373)
         if (rec.b)
-          for (int j = lane; j < m; j += 64) rec.b[base * m + j] = brow[j];
+          for (int j = lane + 64 * role; j < m; j += (PAIR ? 128 : 64)) rec.b[base * m + j] = brow[j];
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
           const int t = 64 * s + lane;
-          if (vmask & (1u << s)) {
+          if ((vmask & (1u << s)) && (!PAIR || (s & 1) == role)) {
             if (rec.z) rec.z[base * nst + t] = (double)((zb >> s) & 1u);
             if (rec.alpha) rec.alpha[base * nst + t] = al[s];
             if (rec.pout) rec.pout[base * nst + t] = po[s];
           }
         }
-        if (lane == 0) {
+        if (lane == 0 && role == 0) {
           if (rec.theta) rec.theta[base] = theta;
           if (rec.nu) rec.nu[base] = nu;
         }
