@@ -2250,6 +2250,9 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
             zb = (zb & ~(1u << s)) | ((unsigned)((xzm[s] >> lane) & 1ull) << s);
           }
         }
+        // the partner's reads complete before either wave can overwrite its slots again
+        // (a later sweep's z stage; a launch's stage mask need not hold a barrier between)
+        __syncthreads();
       }
     }
     fair_prio<OCC>(fair);
@@ -2289,6 +2292,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
 #pragma unroll
           for (int s = 0; s < NS; ++s)
             if ((s & 1) != role) al[s] = xal[s][lane];
+          __syncthreads();   // as for z: reads done before the next write of these slots
         }
       }
     }

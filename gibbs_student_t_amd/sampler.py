@@ -11,7 +11,11 @@ Differences from the reference, all documented in DESIGN.md:
 * variates come from on-device Philox4x32-10 instead of numpy's MT19937 stream, so chains
   are distributionally -- not bitwise -- equal to the reference's for the same seed;
 * the b draw uses the Cholesky square root (mean = cho_solve(Sigma, d), the reference's own
-  expression at gibbs.py:321-322) instead of the SVD one at gibbs.py:169-171.
+  expression at gibbs.py:321-322) instead of the SVD one at gibbs.py:169-171 -- except where
+  Sigma is beyond fp64 resolution (vvh17's all-outlier start): there the reference's SVD
+  returns the small eigenvalues at LAPACK's rounding floor and the kernel draws from
+  Sigma + f I instead (the SVD noise floor, include/gst.h gst_sweep; ``exact_bdraw=True``
+  turns it off).
 """
 from __future__ import annotations
 
@@ -62,6 +66,7 @@ class Gibbs:
                    vary_alpha=vary_alpha, alpha=alpha, pspin=pspin)
         self._cfg = dict(cfg, exact_bdraw=bool(exact_bdraw))
         self._x_all = None
+        self._counter_at_sample = None      # Philox counter when sample() last returned
         self._native = NativeSampler(pta, cfg, device)
         self._native.set_debug(exact_bdraw=exact_bdraw)
         self._native.alloc(C)
@@ -235,6 +240,7 @@ class Gibbs:
                                  (done / niter * 100, time.time() - tstart))
                 sys.stdout.flush()
         x = self._pull()
+        self._counter_at_sample = self._sweep_counter
         return x[0] if C == 1 else x
 
     # ---- checkpoint / resume (not in the reference: gibbs.py:344-350 restarts its chains) --
@@ -246,8 +252,16 @@ class Gibbs:
         by (seed, sweep index, chain)."""
         if self._x_all is None:
             raise RuntimeError("checkpoint() needs a finished sample() call")
+        if self._sweep_counter != self._counter_at_sample:
+            # a stage method advanced the Philox counter after sample() returned, so the x
+            # of that sample() no longer pairs with the counter: a resume from it would not
+            # be the uninterrupted chain
+            raise RuntimeError("checkpoint() must directly follow sample(): "
+                               f"{self._sweep_counter - self._counter_at_sample} stage "
+                               "call(s) ran since")
         return make_checkpoint(self._cfg, self.pta.get_basis()[0].shape, self.seed,
-                               self._sweep_counter, x=self._x_all, b=self._b_all,
+                               self._sweep_counter, fingerprint=dataset_fingerprint(self.pta),
+                               x=self._x_all, b=self._b_all,
                                z=self._z_all, alpha=self._alpha_all, pout=self._pout_all,
                                theta=self._theta_all, nu=self._tdf_all)
 
@@ -262,7 +276,8 @@ class Gibbs:
         if not isinstance(ckpt, dict):
             with np.load(ckpt, allow_pickle=False) as f:
                 ckpt = {k: f[k] for k in f.files}
-        check_checkpoint(ckpt, self._cfg, self.pta.get_basis()[0].shape, self.nchains)
+        check_checkpoint(ckpt, self._cfg, self.pta.get_basis()[0].shape, self.nchains,
+                         fingerprint=dataset_fingerprint(self.pta))
         self.seed = int(ckpt["seed"])
         self._sweep_counter = int(ckpt["sweep_counter"])
         self._b_all = np.array(ckpt["b"], dtype=np.float64)
@@ -272,39 +287,81 @@ class Gibbs:
         self._theta_all = np.array(ckpt["theta"], dtype=np.float64)
         self._tdf_all = np.array(ckpt["nu"], dtype=np.float64)
         self._x_all = np.array(ckpt["x"], dtype=np.float64)
+        self._counter_at_sample = self._sweep_counter
         return self._x_all[0] if self.nchains == 1 else self._x_all
 
     def close(self):
         self._native.close()
 
 
-CKPT_VERSION = 1
+CKPT_VERSION = 2
 _CKPT_OPTS = ("model", "tdf", "m", "vary_df", "theta_prior", "vary_alpha", "alpha", "pspin",
               "exact_bdraw")
+_CKPT_STR_OPTS = ("model", "theta_prior")
 
 
-def make_checkpoint(cfg, basis_shape, seed, sweep_counter, **state):
-    """Checkpoint dict: state arrays (leading chain axis) + key, counter, options, shape."""
+def dataset_fingerprint(pta):
+    """SHA-256 of the data a chain's posterior depends on: residuals, error bars, the basis T
+    and its Fourier frequencies, the timing-model prior, the backend / ECORR assignment.  A
+    checkpoint resumes only on the dataset it was taken on."""
+    import hashlib
+    h = hashlib.sha256()
+    parts = [pta.get_residuals()[0], getattr(pta, "_toaerrs", np.zeros(0)),
+             pta.get_basis()[0], getattr(pta, "Ffreqs", np.zeros(0)),
+             np.array([float(getattr(pta, "tm_weight", 0.0))]),
+             getattr(pta, "bidx", np.zeros(0)), getattr(pta, "ecorr_backend", np.zeros(0))]
+    for a in parts:
+        a = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+        h.update(str(a.shape).encode())
+        h.update(a.tobytes())
+    return h.hexdigest()
+
+
+def _norm_opt(key, v):
+    """Option value in a comparable form: tdf = 4 and 4.0, or np.float64(0.01) and 0.01,
+    are the same option."""
+    if v is None:
+        return None
+    if key in _CKPT_STR_OPTS:
+        return str(v)
+    if isinstance(v, (bool, np.bool_)):
+        return bool(v)
+    return float(v)
+
+
+def _opts_json(cfg):
+    import json
+    return json.dumps({k: _norm_opt(k, cfg.get(k)) for k in _CKPT_OPTS}, sort_keys=True)
+
+
+def make_checkpoint(cfg, basis_shape, seed, sweep_counter, fingerprint="", **state):
+    """Checkpoint dict: state arrays (leading chain axis) + key, counter, options (JSON of
+    normalised values), basis shape and the dataset fingerprint."""
     ck = {k: np.asarray(v, dtype=np.float64) for k, v in state.items()}
     ck.update(version=np.int64(CKPT_VERSION), seed=np.uint64(seed),
               sweep_counter=np.int64(sweep_counter), n=np.int64(basis_shape[0]),
-              m=np.int64(basis_shape[1]),
-              options=np.array([f"{k}={cfg.get(k)!r}" for k in _CKPT_OPTS]))
+              m=np.int64(basis_shape[1]), options=np.array(_opts_json(cfg)),
+              fingerprint=np.array(str(fingerprint)))
     return ck
 
 
-def check_checkpoint(ck, cfg, basis_shape, nchains):
-    """Raise ValueError unless ``ck`` fits a sampler with these options / shape / chains."""
+def check_checkpoint(ck, cfg, basis_shape, nchains, fingerprint=None):
+    """Raise ValueError unless ``ck`` fits a sampler with these options / shape / chains (and,
+    when ``fingerprint`` is given, was taken on the same dataset)."""
+    import json
     if int(ck.get("version", -1)) != CKPT_VERSION:
         raise ValueError(f"checkpoint version {ck.get('version')} != {CKPT_VERSION}")
-    want = [f"{k}={cfg.get(k)!r}" for k in _CKPT_OPTS]
-    got = [str(v) for v in np.asarray(ck["options"]).tolist()]
+    got = json.loads(str(np.asarray(ck["options"])))
+    want = json.loads(_opts_json(cfg))
     if got != want:
-        diff = [(a, b) for a, b in zip(got, want) if a != b]
-        raise ValueError(f"checkpoint model options differ: {diff}")
+        diff = {k: (got.get(k), want.get(k)) for k in want if got.get(k) != want.get(k)}
+        raise ValueError(f"checkpoint model options differ (checkpoint, sampler): {diff}")
     if (int(ck["n"]), int(ck["m"])) != tuple(basis_shape):
         raise ValueError(f"checkpoint basis {int(ck['n'])}x{int(ck['m'])} != "
                          f"{basis_shape[0]}x{basis_shape[1]}")
+    if fingerprint is not None and str(np.asarray(ck["fingerprint"])) != str(fingerprint):
+        raise ValueError("checkpoint was taken on a different dataset (residuals, error bars "
+                         "or basis differ)")
     for k in ("x", "b", "z", "alpha", "pout", "theta", "nu"):
         if np.asarray(ck[k]).shape[0] != nchains:
             raise ValueError(f"checkpoint has {np.asarray(ck[k]).shape[0]} chains, "

@@ -63,9 +63,13 @@ def test_two_waves_match_one_wave(name):
 @pytest.mark.parametrize("mask", [_abi.STAGE_HYPER | _abi.STAGE_B,
                                   _abi.STAGE_B | _abi.STAGE_B_FORCE,
                                   _abi.STAGE_HYPER,
-                                  _abi.STAGE_ALL & ~_abi.STAGE_HYPER])
+                                  _abi.STAGE_ALL & ~_abi.STAGE_HYPER,
+                                  _abi.STAGE_Z, _abi.STAGE_ALPHA,
+                                  _abi.STAGE_Z | _abi.STAGE_ALPHA])
 def test_two_waves_stage_masks(mask):
-    """The drop-in's update_* methods launch stage subsets; each subset must agree too."""
+    """The drop-in's update_* methods launch stage subsets; each subset must agree too --
+    also multi-sweep launches of the z / alpha stages alone, where no other stage's barrier
+    separates one sweep's LDS exchange from the next."""
     ref = load_ref("beta_prior")
     C, S = 64, 6
     init = _init(ref, C, 9)
