@@ -12,9 +12,12 @@ the same prior draws with one b-draw rule:
 
 * ``svd``: the reference's own draw (u (u^T d / s) + u s^-1/2 xi);
 * ``exact``: the exact Cholesky draw from Sigma;
-* ``floorC``: the HIP path's rule (oracle ``Oracle.floor_shift``): exact draw from
-  Sigma + f I with f = C x 2^-52 x the largest pivot (C = 0.75) when the smallest pivot is below
-  1e-14 of it.
+* ``floorC`` / ``floorC@G``: the HIP path's rule (oracle ``Oracle.floor_shift``): exact draw
+  from Sigma + f I with f = C x 2^-52 x the largest pivot when the smallest pivot is below G x
+  2^-52 of it (G defaults to the oracle's FLOOR_GATE).
+
+The ``svd`` variant reproduces the reference's own escape sweeps exactly (checked against
+/root/reference/gibbs.py itself by tools/vvh17_escape_reference.py --check-oracle).
 
 Prints and writes the escape sweep (first sweep whose z has sum < n / 2) per seed, the
 trapped fraction at sweeps 100 / 200 / 500 / 1000, and a two-sample KS test of each
@@ -53,6 +56,11 @@ def _setup(dataset):
     return pta, OutlierModel(**MODELS["vvh17"])
 
 
+import oracle.gibbs_oracle as _go  # noqa: E402
+
+GATE0, C0 = _go.FLOOR_GATE, _go.FLOOR_C
+
+
 def run_one(args):
     variant, seed, sweeps, dataset = args
     warnings.simplefilter("ignore")
@@ -60,12 +68,16 @@ def run_one(args):
     pta, cfg = _setup(dataset)
     orc = go.Oracle(pta, cfg)
     mean = "svd"
-    go.FLOOR_GATE, go.FLOOR_C = 1e-14, 0.75     # pool workers are reused: reset every job
+    go.FLOOR_GATE, go.FLOOR_C = GATE0, C0     # pool workers are reused: reset every job
     if variant == "exact":
         go.FLOOR_GATE = 0.0
         mean = "floor"
     elif variant.startswith("floor"):
-        go.FLOOR_C = float(variant[5:])
+        # floorC or floorC@G: f = C x 2^-52 x the largest pivot, gate G x 2^-52
+        c, _, g = variant[5:].partition("@")
+        go.FLOOR_C = float(c)
+        if g:
+            go.FLOOR_GATE = float(g) * 2.0 ** -52
         mean = "floor"
     np.random.seed(seed)
     x = pta.sample_params()
@@ -98,6 +110,9 @@ def main():
     ap.add_argument("--golden", default=None,
                     help="also write the svd (reference) variant's escape sweeps here "
                          "(tests/golden/vvh17_escape_ref.json)")
+    ap.add_argument("--ref-json", default=None,
+                    help="take the svd variant's escape sweeps from this reference file "
+                         "(tools/vvh17_escape_reference.py --golden) instead of running it")
     ap.add_argument("--golden-from", default=None,
                     help="only write --golden from an earlier --out file")
     a = ap.parse_args()
@@ -106,10 +121,18 @@ def main():
             write_golden(json.load(f), a.golden)
         return
     variants = a.variants.split(",")
-    jobs = [(v, a.seed0 + s, a.sweeps, a.dataset) for v in variants for s in range(a.seeds)]
+    refrows = []
+    if a.ref_json:
+        with open(a.ref_json) as f:
+            rj = json.load(f)
+        assert rj["seed0"] == a.seed0 and rj["seeds"] >= a.seeds and rj["sweeps"] == a.sweeps
+        refrows = [("svd", a.seed0 + i, e, []) for i, e in enumerate(rj["escape"][:a.seeds])]
+        variants = ["svd"] + [v for v in variants if v != "svd"]
+    jobs = [(v, a.seed0 + s, a.sweeps, a.dataset) for v in variants for s in range(a.seeds)
+            if not (a.ref_json and v == "svd")]
     t0 = time.time()
     with Pool(a.procs) as pool:
-        res = pool.map(run_one, jobs, chunksize=1)
+        res = refrows + pool.map(run_one, jobs, chunksize=1)
     from scipy.stats import ks_2samp
     out = {"dataset": a.dataset, "seeds": a.seeds, "seed0": a.seed0, "sweeps": a.sweeps,
            "criterion": "first sweep with sum z < n/2", "variants": {}}
