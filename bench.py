@@ -578,12 +578,18 @@ def main():
     ess = rhat = by_group = None
     stage_ms = None
     win_s = 0.0
+    # b draws at the SVD noise floor (status >> 8 counts them, include/gst.h ABI 5): over the
+    # ESS window, i.e. at stationarity (the timed region starts 5 sweeps after prior draws)
+    floor_win = None
     if ess_win > 0:
         if burn > 0:
             ns.sweep(burn, seed=args.seed, sweep0=W + K, chain0=c0)
+        nfl0 = np.asarray(ns.get_state()["status"]) >> 8
         wrec = ns.alloc_records(ess_win // thin, keys=("x", "theta"))
         win_s = timed(lambda: ns.sweep(ess_win, records=wrec, record_every=thin, seed=args.seed,
                                        sweep0=W + K + burn, chain0=c0))
+        nflw = (np.asarray(ns.get_state()["status"]) >> 8) - nfl0
+        floor_win = np.array([float((nflw > 0).sum()), float(nflw.sum())])
         if not large and not args.stub and not args.no_stage_costs:   # at the working clock
             stage_ms = stage_costs(ns, max(1, min(K, 200)), args.seed, W + K + burn + ess_win,
                                    c0)
@@ -604,8 +610,11 @@ def main():
         stage_ms = stage_costs(ns, max(1, min(K, 200)), args.seed, W + K + burn + ess_win, c0)
     shards = dist.gather_chains(np.array([[c0, c0 + C]], dtype=np.float64), dev)
     m_vec = np.array([elapsed, kernel_ms, win_s])
-    # status bit 4 (16) is informational: a b draw at the SVD noise floor (include/gst.h)
-    s_vec = np.array([float(((status & ~16) != 0).sum()), float(((status & 16) != 0).sum())])
+    # status bit 4 (16) is informational: a b draw at the SVD noise floor (include/gst.h),
+    # bits 8.. count them; every other flag of bits 0-7 is an error
+    s_vec = np.array([float(((status & 0xef) != 0).sum()), float(((status & 16) != 0).sum()),
+                      float((status >> 8).sum())] +
+                     (list(floor_win) if floor_win is not None else [0.0, 0.0]))
     s_vec, m_vec = dist.reduce_summary(s_vec, m_vec, dev)
     elapsed, kernel_ms, win_s = (float(v) for v in m_vec)
 
@@ -738,7 +747,18 @@ def main():
                            "ess_total": ess, "rhat_max": rhat},
             "shards": [[int(a), int(b)] for a, b in shards],   # global chain ids per rank
             "chains_with_status": int(s_vec[0]),
-            "chains_floor_draw": int(s_vec[1]),
+            "chains_floor_draw": ({"ess_window_chains": int(s_vec[3]),
+                                   "ess_window_draws": int(s_vec[4]),
+                                   "ess_window_draws_per_chain_sweep":
+                                       float(s_vec[4]) / (C * world * ess_win),
+                                   "since_start_chains": int(s_vec[1]),
+                                   "since_start_draws": int(s_vec[2]),
+                                   "what": "b draws at the SVD noise floor (include/gst.h): "
+                                           "in the ESS window (stationary) and cumulative "
+                                           "since the prior-draw start (warmup + timed)"}
+                                  if ess_win > 0 else
+                                  {"since_start_chains": int(s_vec[1]),
+                                   "since_start_draws": int(s_vec[2])}),
             "kernel_ms": kernel_ms,
             # the persistent kernel is bound by VALU issue and the latency of the
             # factorisations' step-to-step LDS hand-offs (PMC: MFMA busy ~11%, VALU ~57% of

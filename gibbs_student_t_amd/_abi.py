@@ -24,10 +24,19 @@ DEBUG_LARGE_GRAM = 2
 DEBUG_LARGE_HYPER = 4
 DEBUG_EXACT_BDRAW = 8
 STATUS_FLOOR = 16          # status bit 4: a b draw ran at the SVD noise floor
+STATUS_FLAGS = 0xff        # bits 0-7: flags; bits 8..30: the number of floor draws (ABI 5)
+STATUS_ERRORS = STATUS_FLAGS & ~STATUS_FLOOR   # every flag but the informational floor bit
+STATUS_FLOOR_COUNT_SHIFT = 8
+
+
+def floor_draws(status):
+    """Per chain: the b draws made at the SVD noise floor since status was last zeroed."""
+    import numpy as np
+    return np.asarray(status) >> STATUS_FLOOR_COUNT_SHIFT
 PATHS = {"auto": PATH_AUTO, "persistent": PATH_PERSISTENT, "large": PATH_LARGE}
 KERNEL_KINDS = ("record", "white", "gram", "tmelim", "hyper", "btm", "tb", "toa")
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 EXPORTS = ("gst_version", "gst_tape_stride", "gst_last_error", "gst_ctx_create",
            "gst_ctx_destroy", "gst_model_set", "gst_model_set_batch", "gst_model_info",
            "gst_sweep", "gst_set_path", "gst_get_path", "gst_set_waves", "gst_set_debug", "gst_set_timing", "gst_kernel_times", "gst_eval_lnlike", "gst_sync",

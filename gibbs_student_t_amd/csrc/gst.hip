@@ -579,6 +579,25 @@ static int ensure_scratch(Ctx* cx, int C, hipStream_t st) {
   return 0;
 }
 
+// The red-noise MH block's launches: one per hyper kernel class present (gst_large.hpp
+// hyper_class); a chain of another class returns at once.
+static int launch_hyper(Ctx* cx, gst::LArgs& a, const bool (&hcls)[3], dim3 g8, dim3 b8,
+                        dim3 g16, dim3 b16, dim3 g_chain, dim3 b_chain, hipStream_t st) {
+  if (hcls[0]) {
+    a.kclass = 8;
+    LG_LAUNCH(GST_K_HYPER, gst::lg_hyper_reg<8>, g8, b8, 0);
+  }
+  if (hcls[1]) {
+    a.kclass = 16;
+    LG_LAUNCH(GST_K_HYPER, gst::lg_hyper_reg<16>, g16, b16, 0);
+  }
+  if (hcls[2]) {
+    a.kclass = 0;
+    LG_LAUNCH(GST_K_HYPER, gst::lg_hyper, g_chain, b_chain, cx->lds_hyper);
+  }
+  return 0;
+}
+
 // One sweep = record, white, gram, tmelim, hyper, btm, tb, toa launches (gst_large.hpp).
 static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
                         const gst::DevTape& dt, int C, int nsweeps, long long sweep0,
@@ -592,22 +611,29 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
                eval_only, ow, oh};
   const int nsb = (h.mp / 16 + 3) / 4;
   const int npairs = nsb * (nsb + 1) / 2;
-  const bool small_toa = ys <= gst::TBLK_SMALL_NPAD;
-  // hyper blocks of up to HR_COLS (62) / HR_COLS_WIDE (126) columns: one wave per chain,
-  // register-resident elimination (lg_hyper_reg<8> / <16>); larger ones: lg_hyper (LDS)
-  int hcols = 0;
-  for (const gst::DevModel& hm : cx->hmd) hcols = std::max(hcols, hm.nf + hm.nec);
-  int hr_mt = hcols <= gst::HR_COLS ? 8 : (hcols <= gst::HR_COLS_WIDE ? 16 : 0);
-  if (cx->debug & GST_DEBUG_LARGE_HYPER) hr_mt = 0;
-  const int hr_wpb = hr_mt == 16 ? gst::HR<16>::WPB : gst::HR<8>::WPB;
-  const dim3 g_hr((C + hr_wpb - 1) / hr_wpb), b_hr(64 * hr_wpb);
+  // kernel classes present among the batch's datasets (gst_large.hpp white_class /
+  // toa_class / hyper_class): one launch per class, each chain runs in its own dataset's
+  // class, so its arithmetic never depends on the other datasets of the batch.  Hyper blocks
+  // of up to HR_COLS (62) / HR_COLS_WIDE (126) columns: one wave per chain, register-resident
+  // elimination (lg_hyper_reg<8> / <16>); larger ones: lg_hyper (LDS)
+  const int hyper_lds = (cx->debug & GST_DEBUG_LARGE_HYPER) ? 1 : 0;
+  bool wcls[3] = {false, false, false}, tcls[2] = {false, false}, hcls[3] = {false, false, false};
+  for (const gst::DevModel& hm : cx->hmd) {
+    wcls[gst::white_class(hm.npad)] = true;
+    tcls[gst::toa_class(hm.npad)] = true;
+    const int hc = gst::hyper_class(hm.nf + hm.nec, hyper_lds);
+    hcls[hc == 8 ? 0 : (hc == 16 ? 1 : 2)] = true;
+  }
+  a.hyper_lds = hyper_lds;
+  const dim3 g_hr8((C + gst::HR<8>::WPB - 1) / gst::HR<8>::WPB), b_hr8(64 * gst::HR<8>::WPB);
+  const dim3 g_hr16((C + gst::HR<16>::WPB - 1) / gst::HR<16>::WPB), b_hr16(64 * gst::HR<16>::WPB);
   // Grams of at most GS_NTMAX 16-column tiles: one wave per chain (lg_gram_small<NT>)
   int gram_small = h.mp / 16;
   for (const gst::DevModel& hm : cx->hmd)
     if (hm.mp != h.mp) gram_small = 0;
   if (gram_small > gst::GS_NTMAX || (cx->debug & GST_DEBUG_LARGE_GRAM)) gram_small = 0;
   const dim3 g_gs((C + gst::GS_WPB - 1) / gst::GS_WPB), b_gs(64 * gst::GS_WPB);
-  const dim3 g_chain(C), b_chain(gst::LBLK), b_toa(small_toa ? gst::TBLK_SMALL : gst::TBLK);
+  const dim3 g_chain(C), b_chain(gst::LBLK);
   const dim3 g_gram(npairs * ((C + gst::GRAM_WAVES - 1) / gst::GRAM_WAVES)), b_gram(64 * gst::GRAM_WAVES);
   const dim3 g_tb(ys / 64, (C + 64 * gst::TB_CG - 1) / (64 * gst::TB_CG));
   cx->evused = 0;
@@ -618,12 +644,18 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
   for (int it = 0; it < nit; ++it) {
     a.it = it;
     if (rec_on && it % record_every == 0) LG_LAUNCH(GST_K_RECORD, gst::lg_record, g_chain, b_chain, 0);
-    if (ys <= gst::TBLK_WAVE_NPAD)
+    if (wcls[0]) {
+      a.kclass = 0;
       LG_LAUNCH(GST_K_WHITE, gst::lg_white<gst::TBLK_WAVE>, g_chain, dim3(gst::TBLK_WAVE), 0);
-    else if (small_toa)
-      LG_LAUNCH(GST_K_WHITE, gst::lg_white<gst::TBLK_SMALL>, g_chain, b_toa, 0);
-    else
-      LG_LAUNCH(GST_K_WHITE, gst::lg_white<gst::TBLK>, g_chain, b_toa, 0);
+    }
+    if (wcls[1]) {
+      a.kclass = 1;
+      LG_LAUNCH(GST_K_WHITE, gst::lg_white<gst::TBLK_SMALL>, g_chain, dim3(gst::TBLK_SMALL), 0);
+    }
+    if (wcls[2]) {
+      a.kclass = 2;
+      LG_LAUNCH(GST_K_WHITE, gst::lg_white<gst::TBLK>, g_chain, dim3(gst::TBLK), 0);
+    }
     if ((mask & (6u | GST_STAGE_GRAM)) || eval_only) {
       if (ev_mark(cx, GST_K_GRAM, st, true)) return -1;
       switch (gram_small) {
@@ -641,12 +673,8 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
       if (ev_mark(cx, GST_K_GRAM, st, false)) return -1;
       LG_LAUNCH(GST_K_TMELIM, gst::lg_tmelim, g_chain, b_chain, cx->lds_tm);
       if (!(mask & GST_STAGE_GRAM)) {   // timing diagnostic: Gram + TM elimination only
-        if (hr_mt == 8)
-          LG_LAUNCH(GST_K_HYPER, gst::lg_hyper_reg<8>, g_hr, b_hr, 0);
-        else if (hr_mt == 16)
-          LG_LAUNCH(GST_K_HYPER, gst::lg_hyper_reg<16>, g_hr, b_hr, 0);
-        else
-          LG_LAUNCH(GST_K_HYPER, gst::lg_hyper, g_chain, b_chain, cx->lds_hyper);
+        if (launch_hyper(cx, a, hcls, g_hr8, b_hr8, g_hr16, b_hr16, g_chain, b_chain, st))
+          return -1;
         if (eval_only) break;
         if ((mask & 4u) && !(cx->debug & GST_DEBUG_EXACT_BDRAW)) {
           // the b draw's floor pass (include/gst.h gst_sweep): chains whose Sigma is beyond
@@ -654,12 +682,8 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
           // returns at once (SC_FLOOR == 0)
           a.floor_pass = 1;
           LG_LAUNCH(GST_K_TMELIM, gst::lg_tmelim, g_chain, b_chain, cx->lds_tm);
-          if (hr_mt == 8)
-            LG_LAUNCH(GST_K_HYPER, gst::lg_hyper_reg<8>, g_hr, b_hr, 0);
-          else if (hr_mt == 16)
-            LG_LAUNCH(GST_K_HYPER, gst::lg_hyper_reg<16>, g_hr, b_hr, 0);
-          else
-            LG_LAUNCH(GST_K_HYPER, gst::lg_hyper, g_chain, b_chain, cx->lds_hyper);
+          if (launch_hyper(cx, a, hcls, g_hr8, b_hr8, g_hr16, b_hr16, g_chain, b_chain, st))
+            return -1;
           a.floor_pass = 0;
         }
         if (mask & 4u) {
@@ -669,10 +693,14 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
       }
     }
     if (!eval_only && (mask & 0x78u)) {
-      if (small_toa)
-        LG_LAUNCH(GST_K_TOA, gst::lg_toa<gst::TBLK_SMALL>, g_chain, b_toa, 0);
-      else
-        LG_LAUNCH(GST_K_TOA, gst::lg_toa<gst::TBLK>, g_chain, b_toa, 0);
+      if (tcls[0]) {
+        a.kclass = 0;
+        LG_LAUNCH(GST_K_TOA, gst::lg_toa<gst::TBLK_SMALL>, g_chain, dim3(gst::TBLK_SMALL), 0);
+      }
+      if (tcls[1]) {
+        a.kclass = 1;
+        LG_LAUNCH(GST_K_TOA, gst::lg_toa<gst::TBLK>, g_chain, dim3(gst::TBLK), 0);
+      }
     }
   }
   HIP_OK(hipEventRecord(cx->ev1, st));

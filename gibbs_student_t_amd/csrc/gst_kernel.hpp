@@ -281,17 +281,21 @@ __device__ __forceinline__ double wave_max(double v) {
 // The reference draws b through sl.svd(Sigma) (gibbs.py:169-171).  When Sigma's smallest
 // eigenvalues lie below ~eps ||Sigma|| (vvh17's all-outlier start, alpha = 1e10: cond ~ 1e22,
 // while Sigma diagonally scaled is well conditioned) LAPACK returns them at its own rounding
-// floor, ~0.1-6 x 2^-52 s_max, so its draw is in effect one from Sigma + f I -- which is what
+// floor, ~0.3-2 x 2^-52 s_max, so its draw is in effect one from Sigma + f I -- which is what
 // lets the reference's chains leave that state within ~100 sweeps (the exact draw stays there
 // for thousands).  The b draw reproduces it: when the smallest pivot of
-// the factor over the real columns is below FLOOR_GATE x the largest, b is drawn exactly from
+// the factor over the real columns is below FLOOR_GATE = 2^-52 x the largest (the pivot ratio
+// below which LAPACK's SVD resolves those eigenvalues no longer: above it the reference's SVD
+// mean agrees with the exact mean to ~1e-6), b is drawn exactly from
 // Sigma + f I with f = FLOOR_C 2^-52 x the largest pivot; every other draw is the exact one.
-constexpr double FLOOR_GATE = 1e-14;
+// Each floor draw sets status bit 4 and adds 1 to the floor-draw count in bits 8..30.
+constexpr double FLOOR_GATE = 0x1p-52;
 #ifndef GST_FLOOR_C
 #define GST_FLOOR_C 0.75  // oracle/gibbs_oracle.py FLOOR_C (tools/vvh17_escape.py calibrates it)
 #endif
 constexpr double FLOOR_C = GST_FLOOR_C;
 constexpr int STATUS_FLOOR = 16;
+constexpr int STATUS_FLOOR_COUNT = 256;   // one floor draw, counted in bits 8..30
 constexpr int DEBUG_EXACT_BDRAW = 8;
 
 // Smallest / largest pivot over the real columns of a factor whose pivot of internal column
@@ -1082,7 +1086,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     else
       return md.sig2[64 * s + lane];
   };
-  int status = 0;
+  int status = 0, nfloor = 0;   // nfloor: b draws at the SVD noise floor in this launch
   lds_order();
 
   // y = r - T b (gibbs.py:213,237,272): 8 columns x NS TOA slots of loads in flight
@@ -1952,6 +1956,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         __syncthreads();
         if (fshift == 0.0) break;
         status |= STATUS_FLOOR;
+        ++nfloor;
         owner = -1;   // a final round refactors x (the MH decisions stand)
         init = false;
         j = NHYPER;
@@ -2031,6 +2036,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         fshift = floor_shift(f_apr, lane, md.ntm, md.ntm_pad, md.ntm_pad + md.nf);
         if (__builtin_expect(fshift != 0.0, 0)) {
           status |= STATUS_FLOOR;
+          ++nfloor;
           gram_and_tm(xv);
           lnl_hyper(xv, fb);
           fshift = 0.0;
@@ -2367,7 +2373,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   if (lane == 0) {
     st.theta[c] = theta;
     st.nu[c] = nu;
-    if (st.status) st.status[c] |= status;
+    if (st.status) st.status[c] = (st.status[c] | status) + nfloor * STATUS_FLOOR_COUNT;
   }
 }
 

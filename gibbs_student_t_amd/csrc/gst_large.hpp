@@ -34,10 +34,9 @@ constexpr int LBLK = 256;      // threads of the per-chain kernels (4 waves)
 // threads per chain of the per-TOA passes (lg_white, lg_toa): 16 waves per chain for the
 // 100k-TOA datasets; 4 for datasets of up to TBLK_SMALL_NPAD TOAs, where a pass is a few
 // TOAs per thread and a 16-wave chain spent it in barriers and reductions with one chain per
-// CU.  Chosen from the largest npad of the launch's datasets (never from the chain count):
-// splitting one dataset's chains across launches or ranks does not change them, but the block
-// size sets the reduction order, so a dataset batched with a larger one (> 8k / > 32k TOAs)
-// gives different (equally valid) chains than the same dataset launched alone.
+// CU.  The block size sets the reduction order, so it is chosen PER DATASET (kernel classes
+// below), never from the launch's other datasets or its chain count: a dataset's chains are
+// the same launched alone, batched with any others, or split over launches and ranks.
 constexpr int TBLK = 1024;
 constexpr int TBLK_SMALL = 256;
 constexpr int TBLK_SMALL_NPAD = 32768;
@@ -45,6 +44,20 @@ constexpr int TBLK_SMALL_NPAD = 32768;
 // loads and one wave reduction each, with no workgroup barrier)
 constexpr int TBLK_WAVE = 64;
 constexpr int TBLK_WAVE_NPAD = 8192;
+// Kernel classes of a dataset (the host launches one kernel per class present in a batch;
+// a chain whose dataset is of another class returns at once):
+//   lg_white: 0 = one wave (npad <= TBLK_WAVE_NPAD), 1 = TBLK_SMALL, 2 = TBLK threads;
+//   lg_toa:   0 = TBLK_SMALL, 1 = TBLK threads;
+//   hyper:    8 / 16 = lg_hyper_reg<8 / 16> (hyper block of <= 62 / 126 columns), 0 = lg_hyper.
+__host__ __device__ constexpr int white_class(int npad) {
+  return npad <= TBLK_WAVE_NPAD ? 0 : (npad <= TBLK_SMALL_NPAD ? 1 : 2);
+}
+__host__ __device__ constexpr int toa_class(int npad) { return npad <= TBLK_SMALL_NPAD ? 0 : 1; }
+// hyper class from the dataset's own hyper block nf + nec: lg_hyper_reg<MT> takes up to
+// HR<MT>::RA = 8 MT - 2 columns (62 / 126)
+__host__ __device__ constexpr int hyper_class(int hcols, int force_lds) {
+  return force_lds ? 0 : (hcols <= 8 * 8 - 2 ? 8 : (hcols <= 8 * 16 - 2 ? 16 : 0));
+}
 constexpr int GRAM_WAVES = 8;  // chains per gram workgroup
 constexpr int TM_PW = 16;      // panel width of the timing-model elimination
 constexpr int TM_TILES = 4;   // trailing-update tiles per wave per round (lg_tmelim)
@@ -84,6 +97,8 @@ struct LArgs {
   int eval_only;
   double *out_w, *out_h;
   int floor_pass;  // 1: the b draw's floor pass (lg_tmelim + hyper on chains with SC_FLOOR > 0)
+  int kclass;      // the launched kernel's class (white_class / toa_class / hyper_class)
+  int hyper_lds;   // GST_DEBUG_LARGE_HYPER: every dataset takes lg_hyper (class 0)
 };
 
 // Dataset of chain c (dataset batches: one DevModel per dataset).  Chains of one 16-chain
@@ -277,6 +292,7 @@ __global__ void __launch_bounds__(TB) lg_white(const DevModel* __restrict__ mds,
   if (threadIdx.x == 0 && a.st.dataset && a.st.status &&
       (unsigned)a.st.dataset[c] >= (unsigned)a.st.nd)
     a.st.status[c] |= 4;                          // bad dataset index (ran on dataset 0)
+  if (white_class(md.npad) != a.kclass) return;   // another class's launch runs this chain
   __shared__ double red[TB / 64];
   __shared__ double mhv[NWHITE][4];
   constexpr int WU = TB == 64 ? 8 : 4;   // TOAs per thread per round of the per-TOA loops
@@ -800,6 +816,7 @@ struct HyperLds {
 __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ mds, LArgs a) {
   const int c = blockIdx.x;
   const DevModel& md = mds[ds_of(a, c)];
+  if (hyper_class(md.nf + md.nec, a.hyper_lds) != 0) return;   // a lg_hyper_reg chain
   extern __shared__ double lsm[];
   // the hyper-dependent columns: Fourier (power law) then ECORR epochs (10^(2 ecorr_b))
   const int nf = md.nf + md.nec, K0 = md.ntm_pad, mp = md.mp;
@@ -973,7 +990,9 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
     sc[SC_FB] = (double)fb;
     if (!a.floor_pass) sc[SC_FLOOR] = fs;
     if (a.st.status)
-      a.st.status[c] |= status | ((redraw && fb) ? 2 : 0) | (fs > 0.0 ? STATUS_FLOOR : 0);
+      a.st.status[c] = (a.st.status[c] | status | ((redraw && fb) ? 2 : 0) |
+                        (fs > 0.0 ? STATUS_FLOOR : 0)) +
+                       ((fs > 0.0 && !a.floor_pass) ? STATUS_FLOOR_COUNT : 0);
   }
   if (!redraw || fb || fs > 0.0) return;   // fs > 0: the floor pass draws b
   // b draw, Fourier block: w_k = zraw_k y_k + eta_k, then L^T v = w (raw columns, pivots on
@@ -1041,6 +1060,7 @@ struct HR {
 };
 constexpr int HR_COLS = HR<8>::RA;        // hyper columns (nf + nec) lg_hyper_reg<8> takes
 constexpr int HR_COLS_WIDE = HR<16>::RA;  // ... and lg_hyper_reg<16>
+static_assert(HR_COLS == 8 * 8 - 2 && HR_COLS_WIDE == 8 * 16 - 2, "hyper_class thresholds");
 
 template <int MT>
 __global__ void __launch_bounds__(64 * HR<MT>::WPB) lg_hyper_reg(const DevModel* __restrict__ mds,
@@ -1053,6 +1073,7 @@ __global__ void __launch_bounds__(64 * HR<MT>::WPB) lg_hyper_reg(const DevModel*
   const int c = blockIdx.x * WPB + wv;
   if (c >= a.C) return;
   const DevModel& md = mds[ds_of(a, c)];
+  if (hyper_class(md.nf + md.nec, a.hyper_lds) != MT) return;  // another class's chain
   double* S0R = smem[wv];
   double* colq = S0R + H::S0;
   double* junk = colq + 8 * MT;
@@ -1220,7 +1241,9 @@ __global__ void __launch_bounds__(64 * HR<MT>::WPB) lg_hyper_reg(const DevModel*
     sc[SC_FB] = (double)fb;
     if (!a.floor_pass) sc[SC_FLOOR] = fs;
     if (a.st.status)
-      a.st.status[c] |= status | ((redraw && fb) ? 2 : 0) | (fs > 0.0 ? STATUS_FLOOR : 0);
+      a.st.status[c] = (a.st.status[c] | status | ((redraw && fb) ? 2 : 0) |
+                        (fs > 0.0 ? STATUS_FLOOR : 0)) +
+                       ((fs > 0.0 && !a.floor_pass) ? STATUS_FLOOR_COUNT : 0);
   }
   if (!redraw || fb || fs > 0.0) return;   // fs > 0: the floor pass draws b
   // b draw, hyper block (lg_hyper's back substitution): the raw factor goes to the S0 region
@@ -1445,6 +1468,7 @@ template <int TB>
 __global__ void __launch_bounds__(TB) lg_toa(const DevModel* __restrict__ mds, LArgs a) {
   const int c = blockIdx.x;
   const DevModel& md = mds[ds_of(a, c)];
+  if (toa_class(md.npad) != a.kclass) return;     // another class's launch runs this chain
   __shared__ double red[TB / 64];
   __shared__ double dfb[32];
   const int n = md.n, nst = a.st.nst, m = md.m, tid = threadIdx.x;

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GST_ABI_VERSION 4
+#define GST_ABI_VERSION 5
 
 /* Outlier model kind: Gibbs(model=...) (gibbs.py:9,32,187-226). */
 enum gst_outlier_model {
@@ -118,7 +118,9 @@ typedef struct gst_model_desc {
  *                       chain, the large path runs it on dataset 0;
  *   status & 8 (bit 3)  large path: the chain's aligned 16-chain group mixes datasets;
  *   status & 16 (bit 4) informational: a b draw ran at the SVD noise floor (Sigma beyond
- *                       fp64 resolution, e.g. vvh17's all-outlier start; see gst_sweep).
+ *                       fp64 resolution, e.g. vvh17's all-outlier start; see gst_sweep);
+ *   status >> 8 (ABI 5) the number of b draws made at the SVD noise floor (each adds 256), so
+ *                       that a caller who zeroes status can count them over any window.
  * dataset[C] gives each chain's dataset index into the batch passed to
  * gst_model_set_batch; it may be NULL when there is one dataset. */
 typedef struct gst_state {
@@ -189,10 +191,11 @@ int gst_model_info(void* ctx, int* ndatasets, int* nmax, int* tape_stride);
  * depend on how chains are sharded over launches or GPUs.
  * b draw (gibbs.py:145-182): exact Cholesky draw b = Sigma^-1 d + L^-T eta, except where
  * Sigma is beyond fp64 resolution -- its smallest LDL^T pivot (timing-model-first order, real
- * columns) below 1e-14 of its largest, p_max.  There the reference's sl.svd returns the small
- * eigenvalues at LAPACK's rounding floor (~eps x s_max) and its draw is that of Sigma + f I;
- * this path draws from Sigma + f I with f = 0.75 x 2^-52 p_max (and flags status & 16), which
- * reproduces the reference's escape from vvh17's all-outlier start.
+ * columns) below 2^-52 of its largest, p_max.  There the reference's sl.svd returns the small
+ * eigenvalues at LAPACK's rounding floor (~0.3-2 x 2^-52 x s_max) and its draw is in effect
+ * that of Sigma + f I; this path draws from Sigma + f I with f = 0.75 x 2^-52 p_max (flags
+ * status & 16 and counts the draw in status >> 8), which reproduces the reference's escape
+ * from vvh17's all-outlier start.  ABI 4 gated at 1e-14.
  * GST_DEBUG_EXACT_BDRAW turns the floor off. */
 int gst_sweep(void* ctx, const gst_state* state, const gst_records* rec,
               const gst_tape* tape, int nchains, int nsweeps, long long sweep0,

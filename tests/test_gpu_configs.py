@@ -22,7 +22,7 @@ torch = pytest.importorskip("torch")
 if not torch.cuda.is_available():  # pragma: no cover
     pytest.skip("needs a HIP device", allow_module_level=True)
 
-from gibbs_student_t_amd._abi import STATUS_FLOOR  # noqa: E402
+from gibbs_student_t_amd._abi import STATUS_ERRORS, STATUS_FLOOR  # noqa: E402
 from gibbs_student_t_amd import data, run_sims  # noqa: E402
 from gibbs_student_t_amd.model import PTA  # noqa: E402
 from gibbs_student_t_amd.native import NativeSampler  # noqa: E402
@@ -53,7 +53,7 @@ def test_config3_512_chains_properties():
     ns.sweep(S, records=rec, seed=33, sweep0=burn)
     out = ns.get_state()
     x = rec["x"].cpu().numpy()
-    assert np.all((out["status"] & ~STATUS_FLOOR) == 0)
+    assert np.all((out["status"] & STATUS_ERRORS) == 0)
     assert np.all(np.isfinite(x)) and np.all(np.isfinite(out["b"]))
     lo = np.array([p.pmin for p in pta.params])
     hi = np.array([p.pmax for p in pta.params])
@@ -93,7 +93,7 @@ def test_config4_dof_grid_batch():
     recs, _ = st.run(burn + S, burn=burn, keys=("x", "nu", "theta"))
     out = st.ns.get_state()
     st.close()
-    assert np.all((out["status"] & ~STATUS_FLOOR) == 0)
+    assert np.all((out["status"] & STATUS_ERRORS) == 0)
     assert np.all(np.isfinite(recs["x"]))
     nu_t = {}
     for i, e in enumerate(grid):

@@ -42,7 +42,7 @@ def main():
     for k, (ms, nl) in kt.items():
         print(f"  {k:8s} {ms / max(1, S):9.3f} ms/sweep  ({nl} launches)")
     # status bit 4 (16): b drawn at the SVD noise floor (prior draws near log10_A = -18)
-    assert np.all((ns.get_state()["status"] & ~16) == 0)
+    assert np.all((ns.get_state()["status"] & 0xef) == 0)
 
 
 if __name__ == "__main__":
