@@ -443,6 +443,7 @@ def global_diagnostics(draws: np.ndarray, theta: np.ndarray, dsid: np.ndarray,
     ess = {k: 0.0 for k in keys}
     rhat = {k: 0.0 for k in keys}
     by = {}
+    conv = {}   # per group: ESS over the datasets whose every R-hat <= RHAT_OK, and counts
     for d in np.unique(dsid):
         sel = dsid == d
         series = {nm: draws[sel, :, j] for j, nm in enumerate(names)}
@@ -450,18 +451,29 @@ def global_diagnostics(draws: np.ndarray, theta: np.ndarray, dsid: np.ndarray,
             series["theta"] = theta[sel]
         g = by.setdefault(str(groups[d]), ({k: 0.0 for k in keys}, {k: 0.0 for k in keys})) \
             if groups is not None else None
+        de = {}
+        dr = 0.0
         for k, v in series.items():
             e, r = diag.ess_rhat(v)
             e = e if np.isfinite(e) else 0.0
             r = r if np.isfinite(r) else np.inf
             ess[k] += e
             rhat[k] = max(rhat[k], r)
+            de[k] = e
+            dr = max(dr, r)
             if g is not None:
                 g[0][k] += e
                 g[1][k] = max(g[1][k], r)
+        if groups is not None:
+            cg = conv.setdefault(str(groups[d]), [{k: 0.0 for k in keys}, 0, 0])
+            cg[2] += 1
+            if dr <= RHAT_OK:
+                cg[1] += 1
+                for k, e in de.items():
+                    cg[0][k] += e
     if groups is None:
         return ess, rhat
-    return ess, rhat, by
+    return ess, rhat, by, conv
 
 
 def ess_rate(ess, rhat, seconds):
@@ -575,7 +587,7 @@ def main():
 
     # ---- ESS window: its own burn-in (discarded) and recorded window, timed on its own
     names = [p.name.split("_", 1)[1] for p in wl["ptas"][0].params]
-    ess = rhat = by_group = None
+    ess = rhat = by_group = conv_group = None
     stage_ms = None
     win_s = 0.0
     # b draws at the SVD noise floor (status >> 8 counts them, include/gst.h ABI 5): over the
@@ -605,6 +617,7 @@ def main():
                                      groups)
             ess, rhat = res[0], res[1]
             by_group = res[2] if groups is not None else None
+            conv_group = res[3] if groups is not None else None
         del wrec, draws
     if stage_ms is None and not large and not args.stub and not args.no_stage_costs:
         stage_ms = stage_costs(ns, max(1, min(K, 200)), args.seed, W + K + burn + ess_win, c0)
@@ -741,7 +754,15 @@ def main():
             # share the window's wall time with the others')
             "ess_by_model": None if by_group is None else {
                 g: dict(zip(("ess_per_sec", "reason"), ess_rate(e, r, win_s)),
-                        rhat_max=r) for g, (e, r) in sorted(by_group.items())},
+                        rhat_max=r,
+                        # the model's datasets whose every split R-hat <= RHAT_OK (bimodal
+                        # posteriors put the others' chains in different modes):
+                        # their summed ESS of the slowest parameter over the window's time
+                        converged_datasets={
+                            "datasets": conv_group[g][1], "of": conv_group[g][2],
+                            "ess_per_sec": (min(v for v in conv_group[g][0].values() if v > 0)
+                                            / win_s if conv_group[g][1] else None)})
+                for g, (e, r) in sorted(by_group.items())},
             "ess_window": {"burn_in_sweeps": W + K + burn, "sweeps": ess_win, "thin": thin,
                            "seconds": win_s, "chains": C * world,
                            "ess_total": ess, "rhat_max": rhat},

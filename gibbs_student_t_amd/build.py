@@ -72,12 +72,26 @@ def build(force: bool = False, verbose: bool = True, stamps: bool = False,
         units.append((os.path.join(CSRC, "gst_inst.hip"), ["-DGST_SHAPE=" + ",".join(sh)],
                       os.path.join(objdir, "inst_" + "_".join(sh) + ".o")))
 
+    # incremental (not for force=True): a unit is recompiled when its object is missing, older
+    # than one of its sources, or was built with other flags (a .cmd file beside it)
+    kern_deps = [os.path.join(CSRC, f) for f in ("gst_kernel.hpp", "philox.hpp", "gst_shapes.h")]
+    deps = {"gst.hip": SOURCES + [HEADER],
+            "gst_inst.hip": kern_deps + [os.path.join(CSRC, "gst_inst.hip"), HEADER]}
+
     def compile_one(u):
         src, extra, obj = u
         cmd = base + extra + ["-c", src, "-o", obj]
+        stamp = obj + ".cmd"
+        if not force and os.path.exists(obj) and os.path.exists(stamp) and \
+                open(stamp).read() == " ".join(cmd) and \
+                all(os.path.getmtime(d) <= os.path.getmtime(obj)
+                    for d in deps[os.path.basename(src)]):
+            return obj
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
+        with open(stamp, "w") as f:
+            f.write(" ".join(cmd))
         return obj
 
     jobs = jobs or int(os.environ.get("MAX_JOBS", 0)) or min(8, os.cpu_count() or 1)

@@ -1964,15 +1964,21 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         fshift = 0.0;
       }
     } else if ((mask & (6u | 256u)) || eval_only) {
-      gram_and_tm(xv);
-      if (fail_tm) status |= 1;
-      GST_STAMP(2)
       bool Lvalid = false;
       double l0 = 0.0, p0 = 0.0;
       // GST_STAGE_GRAM (256, timing diagnostic): the Gram and the timing-model elimination only
       const int first = (mask & 256u) ? NHYPER + 1 : (((mask & 2u) || eval_only) ? -1 : NHYPER);
+      // pass 1 (rare): the registers hold the factor at the final x and Sigma is beyond fp64
+      // resolution -- refactor x's Sigma + f I for the b draw (floor_shift; the MH decisions
+      // stand).  One copy of the Gram / hyper-block code serves both passes (an inlined
+      // second copy of it raised the 256-register build's spill)
 #pragma unroll 1
-      for (int step = first; step <= NHYPER; ++step) {
+      for (int pass = 0; pass < 2; ++pass) {
+      gram_and_tm(xv);
+      if (fail_tm) status |= 1;
+      GST_STAMP(2)
+#pragma unroll 1
+      for (int step = pass ? NHYPER : first; step <= NHYPER; ++step) {
         fair_prio<OCC>(fair);
         double qv[4], luacc = 0.0;
         if (step == NHYPER) {
@@ -2024,25 +2030,19 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
           Lvalid = false;
         }
       }
+      if (pass == 1 || eval_only || !redraw || fb || (st.debug & DEBUG_EXACT_BDRAW)) break;
+      fshift = floor_shift(f_apr, lane, md.ntm, md.ntm_pad, md.ntm_pad + md.nf);
+      if (__builtin_expect(fshift == 0.0, 1)) break;
+      status |= STATUS_FLOOR;
+      ++nfloor;
+      Lvalid = false;
+      }
+      fshift = 0.0;
     }
     if (eval_only) return;
     GST_STAMP(3)
 
     bool drew = false;
-    if constexpr (!PAIR) {
-      // the registers hold the factor at the final x: is Sigma beyond fp64 resolution?  Then
-      // refactor x's Sigma + f I (Gram stage + hyper block; the MH decisions stand)
-      if (redraw && !fb && !(st.debug & DEBUG_EXACT_BDRAW)) {
-        fshift = floor_shift(f_apr, lane, md.ntm, md.ntm_pad, md.ntm_pad + md.nf);
-        if (__builtin_expect(fshift != 0.0, 0)) {
-          status |= STATUS_FLOOR;
-          ++nfloor;
-          gram_and_tm(xv);
-          lnl_hyper(xv, fb);
-          fshift = 0.0;
-        }
-      }
-    }
     if (redraw && role == owner) {
       if (fb) {
         status |= 2;

@@ -72,3 +72,24 @@ def test_launcher_fails_fast_when_a_rank_dies():
         except ProcessLookupError:
             alive = False
         assert not alive, f"rank process {pid} left running"
+
+
+def test_global_diagnostics_converged_datasets_per_model():
+    """bench.global_diagnostics with run_sims groups: per model, the ESS of the datasets whose
+    every split R-hat <= 1.01 (config 4's ess_by_model[...]['converged_datasets'])."""
+    import numpy as np
+
+    import bench
+    rng = np.random.default_rng(0)
+    C, S = 16, 400
+    dsid = np.repeat(np.arange(4), C)
+    draws = rng.normal(size=(4 * C, S, 2))
+    draws[dsid == 3, :, 0] += np.where(np.arange(C) < C // 2, 5.0, 0.0)[:, None]  # bimodal
+    theta = rng.uniform(size=(4 * C, S))
+    groups = np.array(["a", "a", "b", "b"])
+    ess, rhat, by, conv = bench.global_diagnostics(draws, theta, dsid, ["p0", "p1"],
+                                                   np.array([True] * 4), groups)
+    assert conv["a"][1:] == [2, 2] and conv["b"][1:] == [1, 2]
+    assert by["b"][1]["p0"] > 1.5 and max(by["a"][1].values()) <= 1.01
+    # the converged datasets' ESS is the per-dataset ESS summed over them
+    assert 0 < conv["b"][0]["p0"] < by["b"][0]["p0"]
