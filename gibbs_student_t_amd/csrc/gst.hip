@@ -183,7 +183,7 @@ int gst_ctx_destroy(void* ctx) {
 // row; a persistent-kernel instance larger than the model leaves unit-prior dummy columns
 // between the Fourier block and the residual row.
 static int pack_dataset(Ctx* cx, const gst_model_desc* d, gst::DevModel& md, int ntm_pad,
-                        int raug) {
+                        int raug, int MT) {
   const int n = d->n, m = d->m, nf = d->nfourier, ntm = d->ntm, P = d->nparams;
   const int nec = d->n_ecorr;
   const int mpad = round_up(raug + 1, 16);
@@ -289,6 +289,55 @@ static int pack_dataset(Ctx* cx, const gst_model_desc* d, gst::DevModel& md, int
   }
   md.sum_lfreq = slf;
   md.sum_ldf = sldf;
+  // Persistent kernel, one backend, <= 8 noise classes: the Gram of the augmented basis per
+  // class, G_k = sum_{t in class k} [T|r]_t [T|r]_t^T (long double, rounded once), in the
+  // kernel's 8x8-cyclic register layout [k][slot][lane], and the augmented rows
+  // [T|r]_t in internal order, stored [t][i % 8][i / 8] (a lane's row entries 8 r + p,
+  // r = 0 .. MT-1, are contiguous: 128-bit loads).  With them a sweep's Gram T^T N^-1 [T|r] is
+  //   sum_k c_k G_k + sum_{t: z_t = 1} c_k(t) (1 / alpha_t - 1) [T|r]_t [T|r]_t^T,
+  // c_k = 1 / (efac^2 sigma_k^2 + 10^(2 equad)): N_t = alpha_t^z_t N0_k(t) (gibbs.py:154,
+  // 297-304), a rank-(outlier count) update instead of the n-TOA MFMA Gram (gst_kernel.hpp
+  // gram_and_tm; the kernel takes it while at most LR_MAX TOAs are flagged).
+  md.Gcls = nullptr;
+  md.Trow = nullptr;
+  if (MT > 0 && ncls > 0 && (d->nbackend <= 1)) {
+    const int W = 8 * MT, NSL = MT * (MT + 1) / 2;
+    std::vector<double> trow((size_t)npad * W, 0.0);
+    for (int t = 0; t < n; ++t)
+      for (int i = 0; i < W; ++i) {
+        double v = 0.0;
+        if (i == raug)
+          v = d->residuals[t];
+        else if (i < mpad && int2ref[i] >= 0)
+          v = d->T[(size_t)t * m + int2ref[i]];
+        trow[(size_t)t * W + (i & 7) * MT + (i >> 3)] = v;   // [t][i % 8][i / 8]
+      }
+    std::vector<long double> acc((size_t)ncls * W * W, 0.0L);
+    for (int t = 0; t < n; ++t) {
+      long double* a = acc.data() + (size_t)cidx[t] * W * W;
+      const double* row = trow.data() + (size_t)t * W;
+      auto at = [&](int i) { return row[(i & 7) * MT + (i >> 3)]; };
+      for (int i = 0; i < W; ++i) {
+        const double ri = at(i);
+        if (ri == 0.0) continue;
+        for (int j = 0; j <= i; ++j) a[(size_t)i * W + j] += (long double)ri * at(j);
+      }
+    }
+    std::vector<double> gcls((size_t)ncls * NSL * 64, 0.0);
+    for (int k = 0; k < ncls; ++k)
+      for (int r = 0; r < MT; ++r)
+        for (int sl = 0; sl <= r; ++sl)
+          for (int l = 0; l < 64; ++l) {
+            const int i = 8 * r + (l >> 3), j = 8 * sl + (l & 7);
+            const long double v = i >= j ? acc[((size_t)k * W + i) * W + j]
+                                         : acc[((size_t)k * W + j) * W + i];
+            gcls[((size_t)k * NSL + gst::SL(r, sl)) * 64 + l] = (double)v;
+          }
+    if (upload(cx, trow.data(), trow.size() * 8, &ptr)) return -1;
+    md.Trow = (const double*)ptr;
+    if (upload(cx, gcls.data(), gcls.size() * 8, &ptr)) return -1;
+    md.Gcls = (const double*)ptr;
+  }
 
   md.n = n;
   md.m = m;
@@ -476,7 +525,8 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
   const int raug_pack = path == GST_PATH_LARGE ? ntm_pad + nf + nec : raug;
   std::vector<gst::DevModel> hmd(nd);
   for (int i = 0; i < nd; ++i)
-    if (pack_dataset(cx, &descs[i], hmd[i], ntm_pad, raug_pack)) {
+    if (pack_dataset(cx, &descs[i], hmd[i], ntm_pad, raug_pack,
+                     path == GST_PATH_PERSISTENT ? MT : 0)) {
       free_model(cx);
       return -1;
     }

@@ -60,6 +60,9 @@ __host__ __device__ constexpr int SL(int r, int s) { return r * (r + 1) / 2 + s;
 // (pairing earlier spills there, and its second wave already covers much of the hand-off
 // latency).
 constexpr int KP_MIN = 4;
+// gram_and_tm's low-rank Gram takes sweeps with at most LR_MAX flagged TOAs (z = 1): past
+// that the n-TOA MFMA Gram is cheaper, and the class Grams' share that cancels grows
+constexpr int LR_MAX = 32;
 // the largest TOA-slot count whose two-chains-per-SIMD build the host picks (wider shapes
 // run one chain per SIMD)
 constexpr int OCC2_NS_MAX = 8;
@@ -98,6 +101,11 @@ struct DevModel {
   const double* csig2;   // [ncls]  sigma^2 of each class
   const double* ccount;  // [ncls]  TOAs per class
   int ncls;              // 0 = per-TOA white likelihood; 1..8 = class path
+  // persistent kernel, ncls > 0 (else null): per-class Grams of [T|r] in the 8x8-cyclic
+  // register layout [ncls][SL(MT,0)][64] and the augmented rows [npad][8 MT] (internal
+  // order), for the low-rank Gram (gram_and_tm)
+  const double* Gcls;
+  const double* Trow;
   int n, m, mp, nf, ntm, ntm_pad, raug, nks, npad, nslot_toa;
   int P;
   int idx_efac, idx_equad, idx_logA, idx_gamma;
@@ -1310,6 +1318,63 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     rNr = wave_sum(sr);
     lds_order();
     GST_SUB_BEGIN
+    // Low-rank Gram (one backend, <= 8 noise classes, at most LR_MAX flagged TOAs): the
+    // weights are c_k (1 / alpha_t)^z_t with c_k = 1 / N0 of the TOA's noise class, so
+    //   G = sum_k c_k G_k + sum_{t: z_t = 1} c_k(t) (1 / alpha_t - 1) [T|r]_t [T|r]_t^T
+    // with the per-class Grams G_k of the dataset (DevModel::Gcls) -- the same T^T N^-1 [T|r]
+    // (gibbs.py:302-304) at a cost of the class terms plus one rank-1 update per flagged TOA
+    // instead of the MFMA Gram over all n TOAs (config 2: ~7 flagged of 130).
+    int nout = 0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) nout += __popcll(__ballot(((zb & vmask) >> s) & 1u));
+    if (md.Gcls && nout <= LR_MAX) {
+#pragma unroll
+      for (int i = 0; i < SL(MT, 0); ++i) L[i] = 0.0;
+#pragma unroll 1
+      for (int k = 0; k < md.ncls; ++k) {
+        const double ck = 1.0 / (ef2 * md.csig2[k] + Q);
+        const GDouble* gk = (const GDouble*)md.Gcls + (size_t)k * SL(MT, 0) * 64 + lane;
+#pragma unroll
+        for (int i = 0; i < SL(MT, 0); ++i) L[i] = fma(ck, gk[64 * i], L[i]);
+      }
+      // flagged TOAs, one rank-1 update each: c_k (1 / alpha_t - 1) = w_t - c_k, with the
+      // weight w_t = 1 / N_t the loop above left in vbuf
+#pragma unroll 1
+      for (int s = 0; s < NS; ++s) {
+        unsigned long long bm = __ballot(((zb & vmask) >> s) & 1u);
+#pragma unroll 1
+        while (bm) {
+          const int t = 64 * s + __builtin_ctzll(bm);
+          bm &= bm - 1;
+          const int k = md.ncls > 1 ? md.cidx[t] : 0;
+          const double v = vbuf[t] - 1.0 / (ef2 * md.csig2[k] + Q);
+          // [T|r]_t at internal columns 8 r + p (row side) and 8 r + q (column side): each
+          // lane's MT entries are contiguous in Trow ([t][i % 8][i / 8]), 128-bit loads
+          typedef double v2_t __attribute__((ext_vector_type(2)));
+          const GDouble* tr = (const GDouble*)md.Trow + (size_t)t * 8 * MT;
+          const __attribute__((address_space(1))) v2_t* trp =
+              (const __attribute__((address_space(1))) v2_t*)(tr + MT * p);
+          const __attribute__((address_space(1))) v2_t* trq =
+              (const __attribute__((address_space(1))) v2_t*)(tr + MT * q);
+          double tp_[MT], tq_[MT];
+#pragma unroll
+          for (int r = 0; r < MT; r += 2) {
+            const v2_t a = trp[r / 2], b = trq[r / 2];
+            tp_[r] = a[0];
+            tp_[r + 1] = a[1];
+            tq_[r] = b[0];
+            tq_[r + 1] = b[1];
+          }
+#pragma unroll
+          for (int r = 0; r < MT; ++r) {
+            const double vr = v * tp_[r];
+#pragma unroll
+            for (int s2 = 0; s2 <= r; ++s2) L[SL(r, s2)] = fma(vr, tq_[s2], L[SL(r, s2)]);
+          }
+        }
+      }
+      GST_SUB_END(9)
+    } else {
     if constexpr (PAIR) {
     // Two waves per chain (PAIR): wave 0 computes the
     // even Gram tiles, wave 1 the odd ones (each its own MFMA pipe), then the tiles are swapped
@@ -1486,6 +1551,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
           }
         lds_order();
       }
+    }
     }
     }
     // timing-model prior (1/tm_weight) on its diagonal; unit pivots on the pad columns

@@ -319,9 +319,9 @@ __global__ void __launch_bounds__(TB) lg_white(const DevModel* __restrict__ mds,
 #pragma unroll
       for (int k = 0; k < WU; ++k) {
         const int t = t0 + k * TB < n ? t0 + k * TB : min((int)threadIdx.x, n - 1);  // in-bounds, masked below
-        zv[k] = __builtin_nontemporal_load(zc + t);
-        av[k] = __builtin_nontemporal_load(alc + t);
-        yw[k] = __builtin_nontemporal_load(yc + t);
+        zv[k] = zc[t];
+        av[k] = alc[t];
+        yw[k] = yc[t];
       }
 #pragma unroll
       for (int k = 0; k < WU; ++k) {
@@ -356,10 +356,7 @@ __global__ void __launch_bounds__(TB) lg_white(const DevModel* __restrict__ mds,
           for (int k = 0; k < U; ++k) {
             const int t = t0 + k * TB < n ? t0 + k * TB : min((int)threadIdx.x, n - 1);  // in-bounds, masked below
             sv[k] = s2[t];
-            // the chain's own y^2 / a row streams through once per pass (0.8 MB per chain at
-            // config 5, far beyond L2): a non-temporal load, so that it does not evict the
-            // dataset's sigma^2 row every chain of the XCD re-reads each pass
-            wv[k] = __builtin_nontemporal_load(w2 + t);
+            wv[k] = w2[t];
           }
 #pragma unroll
           for (int k = 0; k < U; ++k) {
@@ -417,9 +414,9 @@ __global__ void __launch_bounds__(TB) lg_white(const DevModel* __restrict__ mds,
 #pragma unroll
     for (int k = 0; k < WU; ++k) {
       const int t = t0 + k * TB < n ? t0 + k * TB : min((int)threadIdx.x, n - 1);  // in-bounds, masked below
-      zv[k] = __builtin_nontemporal_load(zc + t);   // the chain's rows: streamed once
-      av[k] = __builtin_nontemporal_load(alc + t);
-      sv[k] = wf.s2[t];                              // the dataset's rows: L2-shared
+      zv[k] = zc[t];
+      av[k] = alc[t];
+      sv[k] = wf.s2[t];
       rv[k] = md.resid[t];
       bv[k] = wf.nb > 1 ? wf.bk[t] : 0;
     }
