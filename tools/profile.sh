@@ -4,13 +4,13 @@
 # 500-sweep headline run, PMC passes of config 2 and of config 5 (one counter group per run);
 # then: python tools/pmc_json.py gpurun_out/prof_$ROUND 200 2048 > profiles/${ROUND}_pmc_config2.json
 source tools/gpu_step.sh
-O=gpurun_out/prof_${ROUND:-r4}; mkdir -p $O
+O=gpurun_out/prof_${ROUND:-r5}; mkdir -p $O
 step 300 $O/bench_driver.json python bench.py --steps 20 --warmup 5
 B="python bench.py --no-cpu-baseline"
 step 300 $O/bench_s500.json $B --steps 500 --warmup 100
 step 300 $O/bench_c1024.json $B --steps 500 --warmup 100 --chains 1024
 step 200 $O/bench_c3.json $B --config 3 --steps 500 --warmup 100
-step 300 $O/bench_c4.json $B --config 4 --steps 200 --warmup 50
+step 400 $O/bench_c4.json $B --config 4 --steps 200 --warmup 50 --ess-window 20000
 step 300 $O/bench_c5.json $B --config 5 --steps 3 --warmup 1
 step 150 $O/ks.log rocprofv3 --kernel-trace --stats -d $O/ks -o ks --output-format csv -- \
   python bench.py --no-cpu-baseline --no-stage-costs --steps 500 --warmup 100 --ess-window 0

@@ -26,6 +26,8 @@ def main():
     ns = NativeSampler(pta, CFG, 0)
     ns.alloc(C)
     ns.set_state(**initial_state(pta, C, 0))
+    if os.environ.get("RL_EXACT"):   # no SVD-floor pass (GST_DEBUG_EXACT_BDRAW)
+        ns.set_debug(exact_bdraw=True)
     W = int(sys.argv[6]) if len(sys.argv) > 6 else 0
     if W:   # untimed warmup sweeps (the clock ramps out of idle over the first milliseconds)
         ns.sweep(W, seed=1)
