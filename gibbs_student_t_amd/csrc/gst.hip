@@ -881,7 +881,7 @@ int gst_set_debug(void* ctx, int flags) {
   Ctx* cx = static_cast<Ctx*>(ctx);
   if (!cx) return fail("gst_set_debug: null ctx");
   if (flags & ~(GST_DEBUG_POISON | GST_DEBUG_LARGE_GRAM | GST_DEBUG_LARGE_HYPER |
-                GST_DEBUG_EXACT_BDRAW))
+                GST_DEBUG_EXACT_BDRAW | GST_DEBUG_MFMA_GRAM))
     return fail("gst_set_debug: unknown flag");
   cx->debug = flags;
   return 0;

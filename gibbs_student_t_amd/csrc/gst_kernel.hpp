@@ -67,7 +67,10 @@ constexpr int LR_MAX = 32;
 // run one chain per SIMD)
 constexpr int OCC2_NS_MAX = 8;
 __host__ __device__ constexpr int pair_pw(int MT) { return MT - KP_MIN; }
-__host__ __device__ constexpr int kp_for(int OCC) { return OCC == 2 ? 6 : KP_MIN; }
+#ifndef GST_KP_OCC2
+#define GST_KP_OCC2 6   // A/B builds override it (GST_EXTRA_CFLAGS=-DGST_KP_OCC2=...)
+#endif
+__host__ __device__ constexpr int kp_for(int OCC) { return OCC == 2 ? GST_KP_OCC2 : KP_MIN; }
 // index of slot (r, s), s < K0, among the timing-model factor slots (column-major)
 __host__ __device__ constexpr int tm_slot(int MT, int r, int s) {
   return s * MT - s * (s - 1) / 2 + (r - s);
@@ -305,6 +308,7 @@ constexpr double FLOOR_C = GST_FLOOR_C;
 constexpr int STATUS_FLOOR = 16;
 constexpr int STATUS_FLOOR_COUNT = 256;   // one floor draw, counted in bits 8..30
 constexpr int DEBUG_EXACT_BDRAW = 8;
+constexpr int DEBUG_MFMA_GRAM = 16;   // persistent kernel: no low-rank Gram (tests, A/B)
 
 // Smallest / largest pivot over the real columns of a factor whose pivot of internal column
 // j = 64 sl + lane is apr[sl]; real columns are [0, ntm) and [f0, f1) (the rest are unit-prior
@@ -1327,7 +1331,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     int nout = 0;
 #pragma unroll
     for (int s = 0; s < NS; ++s) nout += __popcll(__ballot(((zb & vmask) >> s) & 1u));
-    if (md.Gcls && nout <= LR_MAX) {
+    if (md.Gcls && nout <= LR_MAX && !(st.debug & DEBUG_MFMA_GRAM)) {
 #pragma unroll
       for (int i = 0; i < SL(MT, 0); ++i) L[i] = 0.0;
 #pragma unroll 1

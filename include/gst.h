@@ -245,11 +245,16 @@ int gst_set_waves(void* ctx, int waves);
  * rounding.  Test switches (the defaults are the faster kernels). */
 /* GST_DEBUG_EXACT_BDRAW: every b draw is the exact draw from Sigma, also beyond fp64
  * resolution (no SVD noise floor, see gst_sweep). */
+/* GST_DEBUG_MFMA_GRAM (ABI 5): the persistent kernel computes every Gram on the MFMA path,
+ * never the low-rank one (datasets of <= 8 noise classes, at most 32 flagged TOAs: the
+ * per-class Grams plus one rank-1 update per flagged TOA); the two agree
+ * to rounding. */
 enum gst_debug {
   GST_DEBUG_POISON = 1,
   GST_DEBUG_LARGE_GRAM = 2,
   GST_DEBUG_LARGE_HYPER = 4,
-  GST_DEBUG_EXACT_BDRAW = 8
+  GST_DEBUG_EXACT_BDRAW = 8,
+  GST_DEBUG_MFMA_GRAM = 16
 };
 int gst_set_debug(void* ctx, int flags);
 
