@@ -665,7 +665,7 @@ def main():
         # WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction) at 2048 chains: a rocprofv3
         # --pmc pass of this same command, stored under profiles/ -- NOT measured in this
         # run (counters need their own profiler pass); the newest profile is used
-        for pf in ("r4_pmc_config2.json", "r3_pmc_config2.json", "r2b_pmc_config2.json"):
+        for pf in ("r5_pmc_config2.json", "r4_pmc_config2.json", "r3_pmc_config2.json"):
             pmc = os.path.join(ROOT, "profiles", pf)
             if os.path.exists(pmc) and args.config == 2 and not args.stub:
                 try:
@@ -677,7 +677,7 @@ def main():
                     break
                 except Exception:
                     traffic = None
-        for pf in ("r4_pmc_config5.json", "r3_pmc_config5.json", "pmc_config5.json"):
+        for pf in ("r5_pmc_config5.json", "r4_pmc_config5.json", "r3_pmc_config5.json"):
             pmc5 = os.path.join(ROOT, "profiles", pf)
             if large and args.config == 5 and os.path.exists(pmc5):
                 try:   # HBM bytes per Gram launch (PMC passes of tools/run_large.py, same shape)
