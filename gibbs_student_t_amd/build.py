@@ -37,7 +37,7 @@ def shapes():
     """The persistent kernel's shapes, from the GST_SHAPES list in csrc/gst_shapes.h."""
     txt = open(os.path.join(CSRC, "gst_shapes.h")).read()
     body = txt[txt.index("#define GST_SHAPES(X)"):txt.index("#define GST_PICK_NAME")]
-    return re.findall(r"X\((\d+), (\d+), (\d+), (\d+)\)", body)
+    return re.findall(r"X\((\d+), (\d+), (\d+), (\d+), (\d)\)", body)
 
 
 def build(force: bool = False, verbose: bool = True, stamps: bool = False,

@@ -41,6 +41,7 @@ struct Ctx {
   gst::DevModel* dmd = nullptr;    // device array [nd] (in allocs)
   int nd = 0, nmax = 0, m = 0, raug = 0;
   int MT = 0, NS = 0, K0 = 0, WPB = 4;
+  bool gen = false;                // persistent path: the general white-noise instances
   int ncu = 256;                   // compute units of the device (workgroup sizing)
   double* tmfac = nullptr;         // persistent path: timing-model factor scratch
   unsigned long long* prog = nullptr;  // persistent path: launch-wide sweep counter (fair_prio)
@@ -110,9 +111,12 @@ using gst::kfn_t;
 // occ2: the two-chains-per-SIMD build (256 registers per lane), picked when the launch has
 // more chains than SIMDs; with at most one chain per SIMD the uncapped build keeps more of
 // each chain in registers.  pair: two waves per chain (gst_set_waves).
-kfn_t pick(int MT, int NS, int K0, int RA, bool tape, int wpb, bool occ2, bool pair = false) {
-#define GST_CASE(mt, ns, k0, ra) \
-  if (MT == mt && NS == ns && K0 == k0 && RA == ra) return gst::GST_PICK_NAME(mt, ns, k0, ra)(tape, wpb, occ2, pair);
+// gen: the general white-noise model's instances (GEN shapes).
+kfn_t pick(int MT, int NS, int K0, int RA, bool gen, bool tape, int wpb, bool occ2,
+           bool pair = false) {
+#define GST_CASE(mt, ns, k0, ra, g)                                              \
+  if (MT == mt && NS == ns && K0 == k0 && RA == ra && (gen ? 1 : 0) == g)        \
+    return gst::GST_PICK_NAME(mt, ns, k0, ra, g)(tape, wpb, occ2, pair);
   GST_SHAPES(GST_CASE)
 #undef GST_CASE
   return nullptr;
@@ -120,14 +124,19 @@ kfn_t pick(int MT, int NS, int K0, int RA, bool tape, int wpb, bool occ2, bool p
 
 // Register-resident shapes (MT, K0, RA), smallest first: a model with nf Fourier and ntm
 // timing-model columns runs in the first with 8 K0 >= ntm and RA - 8 K0 >= nf, padded.
+// General white-noise models (GEN) have their own shapes; nf counts the Fourier and the ECORR
+// columns there (both sit in the hyper block).
 struct Shape {
   int MT, K0, RA;
 };
 const Shape kShapes[] = {{8, 2, 56}, {10, 2, 76}, {10, 3, 76}};
+const Shape kShapesGen[] = {{8, 2, 62}, {10, 2, 76}};
 
-const Shape* shape_for(int nf, int ntm) {
-  for (const Shape& sh : kShapes)
-    if (8 * sh.K0 >= (ntm > 0 ? ntm : 1) && sh.RA - 8 * sh.K0 >= nf) return &sh;
+const Shape* shape_for(int nf, int ntm, bool gen = false) {
+  const Shape* tab = gen ? kShapesGen : kShapes;
+  const int nt = gen ? (int)(sizeof kShapesGen / sizeof(Shape)) : (int)(sizeof kShapes / sizeof(Shape));
+  for (int i = 0; i < nt; ++i)
+    if (8 * tab[i].K0 >= (ntm > 0 ? ntm : 1) && tab[i].RA - 8 * tab[i].K0 >= nf) return &tab[i];
   return nullptr;
 }
 
@@ -229,17 +238,21 @@ static int pack_dataset(Ctx* cx, const gst_model_desc* d, gst::DevModel& md, int
     ldf[k] = std::log(d->ffreqs[2 * pair] - prev);
   }
   // noise classes: TOAs with bit-identical sigma share N0 in the white likelihood
+  // (and equal backend: N0 = efac_b^2 sigma^2 + 10^(2 equad_b) depends on both)
   std::vector<double> csig2;
   std::vector<double> ccount;
+  std::vector<int> cback;
   std::vector<int> cidx(npad, -1);
   for (int t = 0; t < n; ++t) {
     const double v = d->toaerrs[t] * d->toaerrs[t];
+    const int bt = (d->nbackend > 1 && d->backend) ? d->backend[t] : 0;
     int u = 0;
-    while (u < (int)csig2.size() && csig2[u] != v) ++u;
+    while (u < (int)csig2.size() && (csig2[u] != v || cback[u] != bt)) ++u;
     if (u == (int)csig2.size()) {
       if (csig2.size() >= 8) break;
       csig2.push_back(v);
       ccount.push_back(0.0);
+      cback.push_back(bt);
     }
     cidx[t] = u;
     ccount[u] += 1.0;
@@ -279,6 +292,7 @@ static int pack_dataset(Ctx* cx, const gst_model_desc* d, gst::DevModel& md, int
   if (upload(cx, ref2int.data(), ref2int.size() * sizeof(int), &ptr)) return -1;
   md.ref2int = (const int*)ptr;
   md.ncls = ncls;
+  for (int u = 0; u < 8; ++u) md.cls_b[u] = u < ncls ? cback[u] : 0;
   if (ncls > 0) {
     if (upload(cx, cidx.data(), cidx.size() * sizeof(int), &ptr)) return -1;
     md.cidx = (const int*)ptr;
@@ -289,18 +303,18 @@ static int pack_dataset(Ctx* cx, const gst_model_desc* d, gst::DevModel& md, int
   }
   md.sum_lfreq = slf;
   md.sum_ldf = sldf;
-  // Persistent kernel, one backend, <= 8 noise classes: the Gram of the augmented basis per
+  // Persistent kernel, <= 8 noise classes: the Gram of the augmented basis per
   // class, G_k = sum_{t in class k} [T|r]_t [T|r]_t^T (long double, rounded once), in the
   // kernel's 8x8-cyclic register layout [k][slot][lane], and the augmented rows
   // [T|r]_t in internal order, stored [t][i % 8][i / 8] (a lane's row entries 8 r + p,
   // r = 0 .. MT-1, are contiguous: 128-bit loads).  With them a sweep's Gram T^T N^-1 [T|r] is
   //   sum_k c_k G_k + sum_{t: z_t = 1} c_k(t) (1 / alpha_t - 1) [T|r]_t [T|r]_t^T,
-  // c_k = 1 / (efac^2 sigma_k^2 + 10^(2 equad)): N_t = alpha_t^z_t N0_k(t) (gibbs.py:154,
+  // c_k = 1 / (efac_b^2 sigma_k^2 + 10^(2 equad_b)): N_t = alpha_t^z_t N0_k(t) (gibbs.py:154,
   // 297-304), a rank-(outlier count) update instead of the n-TOA MFMA Gram (gst_kernel.hpp
   // gram_and_tm; the kernel takes it while at most LR_MAX TOAs are flagged).
   md.Gcls = nullptr;
   md.Trow = nullptr;
-  if (MT > 0 && ncls > 0 && (d->nbackend <= 1)) {
+  if (MT > 0 && ncls > 0) {
     const int W = 8 * MT, NSL = MT * (MT + 1) / 2;
     std::vector<double> trow((size_t)npad * W, 0.0);
     for (int t = 0; t < n; ++t)
@@ -461,6 +475,12 @@ static bool classic(const gst_model_desc* d) {
   return (d->nbackend <= 1) && d->n_ecorr == 0 && d->nparams <= 4 && d->n_hyper <= 4 &&
          d->n_white <= 4;
 }
+// The general white-noise model its GEN instances take: per-backend efac / equad (<= 8
+// backends), ECORR epoch columns in the hyper block, up to 8 parameters.
+static bool general_fits(const gst_model_desc* d) {
+  return d->nparams <= 8 && d->n_hyper <= 8 && d->n_white <= 8 &&
+         (d->nbackend > 0 ? d->nbackend : 1) <= gst::NBMAX;
+}
 
 // Datasets of one batch share the sampler structure: basis shape, parameter roles and the
 // MH index sets.  n (ragged run_sims datasets), the data and the outlier model may differ.
@@ -492,25 +512,28 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
   }
   const gst_model_desc* d = &descs[0];
   const int nf = d->nfourier, ntm = d->ntm, m = d->m, nec = d->n_ecorr;
-  const Shape* sh = shape_for(nf, ntm);
+  const bool gen = !classic(d) && general_fits(d);
+  const Shape* sh = shape_for(nf + (gen ? nec : 0), ntm, gen);
   const int MT = sh ? sh->MT : 0, K0 = sh ? sh->K0 : 0;
   const int raug = sh ? sh->RA : 0;
   const int nsl = (nmax + 63) / 64;
   // TOA slots of 64 held in registers: 2, 3, 4 (J1713-sized), 6, 8 (mid-size, n <= 512),
   // 12, 16 (wide mid-size, n <= 1024: the run_sims model's shape only; these keep one chain
   // per SIMD, their two-chains-per-SIMD builds would spill kilobytes per lane)
-  const int NS = nsl <= 2 ? 2 : (nsl <= 3 ? 3 : (nsl <= 4 ? 4 : (nsl <= 6 ? 6 : (nsl <= 8 ? 8 :
-                 (nsl <= 12 ? 12 : 16)))));
-  const bool fits = sh && classic(d) && round_up(nmax, 4) <= 64 * NS &&
-                    pick(MT, NS, K0, raug, false, 4, false);
+  // (the general white-noise model: 2, 4, 8)
+  const int NS = gen ? (nsl <= 2 ? 2 : (nsl <= 4 ? 4 : 8)) :
+                 (nsl <= 2 ? 2 : (nsl <= 3 ? 3 : (nsl <= 4 ? 4 : (nsl <= 6 ? 6 : (nsl <= 8 ? 8 :
+                 (nsl <= 12 ? 12 : 16))))));
+  const bool fits = sh && (classic(d) || gen) && round_up(nmax, 4) <= 64 * NS &&
+                    pick(MT, NS, K0, raug, gen, false, 4, false);
   int path = cx->path_req;
   if (path == GST_PATH_AUTO) path = fits ? GST_PATH_PERSISTENT : GST_PATH_LARGE;
   if (path == GST_PATH_PERSISTENT && !fits) {
     char b[220];
     std::snprintf(b, sizeof b,
                   "gst_model_set: no persistent-kernel instance for MT=%d NS=%d K0=%d RA=%d "
-                  "(n=%d m=%d nfourier=%d ntm=%d); use the large path", MT, NS, K0, raug,
-                  nmax, m, nf, ntm);
+                  "GEN=%d (n=%d m=%d nfourier=%d ntm=%d n_ecorr=%d); use the large path", MT, NS,
+                  K0, raug, gen ? 1 : 0, nmax, m, nf, ntm, nec);
     return fail(b);
   }
   if (path == GST_PATH_LARGE) {
@@ -542,6 +565,7 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
   cx->raug = raug;
   cx->m = m;
   cx->WPB = 4;
+  cx->gen = path == GST_PATH_PERSISTENT && gen;
   cx->path = path;
   if (path == GST_PATH_LARGE) {
     const gst::DevModel& h = hmd[0];
@@ -789,9 +813,13 @@ static int launch(Ctx* cx, const gst_state* s, const gst_records* r, const gst_t
     else if (wpb >= 2 && C <= 2 * cx->ncu) wpb = 2;
   }
   // two waves per chain when every chain would otherwise leave a SIMD idle
-  const bool pair = !tape && !eval_only && !(mask & GST_STAGE_GRAM) &&
+  // (not for the general white-noise model: its instances run one wave per chain)
+  if (cx->gen && cx->waves == GST_WAVES_TWO)
+    return fail("gst: two waves per chain are not built for the general white-noise model "
+                "(per-backend white noise / ECORR); use GST_WAVES_AUTO or GST_WAVES_ONE");
+  const bool pair = !cx->gen && !tape && !eval_only && !(mask & GST_STAGE_GRAM) &&
                     (cx->waves == GST_WAVES_TWO || (cx->waves == GST_WAVES_AUTO && C <= 2 * cx->ncu));
-  kfn_t k = pick(cx->MT, cx->NS, cx->K0, cx->raug, tape, wpb,
+  kfn_t k = pick(cx->MT, cx->NS, cx->K0, cx->raug, cx->gen, tape, wpb,
                  C > 4 * cx->ncu && cx->NS <= gst::OCC2_NS_MAX, pair);
   if (!k) return fail("gst: no kernel instance");
   // timing-model factor scratch: [C][waves per chain][slots with s < K0][64] doubles

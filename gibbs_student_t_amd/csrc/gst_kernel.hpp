@@ -39,7 +39,8 @@ typedef __attribute__((address_space(1))) double GDouble;
 
 constexpr int NWHITE = 20;
 constexpr int NHYPER = 10;
-constexpr int PMAX = 16;   // sampled parameters (large path; the persistent kernel takes <= 4)
+constexpr int PMAX = 16;   // sampled parameters (large path; the persistent kernel takes <= 4,
+                           // its general-white-noise (GEN) instances <= 8)
 constexpr int NBMAX = 8;   // backends with their own white-noise / ECORR parameters
 __host__ __device__ constexpr int SL(int r, int s) { return r * (r + 1) / 2 + s; }
 
@@ -115,11 +116,12 @@ struct DevModel {
   double efac_const;
   double pmin[PMAX], pmax[PMAX], lp_in[PMAX], lp_sum;
   int hind[PMAX], nh, wind[PMAX], nw;
-  // general white noise (large path; the persistent kernel runs nb == 1, nec == 0):
+  // general white noise (large path; the persistent kernel's GEN instances):
   // per-backend efac / log10_equad / log10_ecorr parameter indices (-1: constant / none),
   // the backend of every TOA, and the ECORR epoch columns (internal columns
   // ntm_pad + nf .. ntm_pad + nf + nec - 1, between the Fourier block and the residual row)
   int nb;
+  int cls_b[8];             // backend of each noise class (classes: equal sigma AND backend)
   const int* bk;            // [npad] backend of each TOA (null when nb == 1)
   int efac_b[NBMAX], equad_b[NBMAX], ecorr_b[NBMAX];
   int nec;
@@ -371,8 +373,32 @@ __device__ __forceinline__ double pget(const double (&x)[4], int i) {
   asm("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
   return i == 0 ? a : (i == 1 ? b : (i == 2 ? c : d));
 }
+// the general-white-noise instances (GEN): up to 8 parameters
+__device__ __forceinline__ double pget(const double (&x)[8], int i) {
+  double v[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    v[k] = x[k];
+    asm("" : "+v"(v[k]));
+  }
+  double r = v[7];
+#pragma unroll
+  for (int k = 6; k >= 0; --k) r = (i == k) ? v[k] : r;
+  return r;
+}
 __device__ __forceinline__ int iget4(const int* a, int i) {   // a[i], i < 4
   return i == 0 ? a[0] : (i == 1 ? a[1] : (i == 2 ? a[2] : a[3]));
+}
+template <int N>
+__device__ __forceinline__ int iget(const int* a, int i) {   // a[i], i < N (4 or 8)
+  if constexpr (N == 4) {
+    return iget4(a, i);
+  } else {
+    int r = a[N - 1];
+#pragma unroll
+    for (int k = N - 2; k >= 0; --k) r = (i == k) ? a[k] : r;
+    return r;
+  }
 }
 
 // The jump (xi * sigma) * scale exactly as numpy evaluates it (gibbs.py:97,130): no FMA
@@ -962,13 +988,18 @@ __device__ __forceinline__ void chol_stats(CholCtx& cc) {
 // next proposal, and the one after it on the branch the chain's acceptance history predicts
 // -- and exchange the lnL values through LDS, so that a round settles one or two MH steps
 // (DESIGN.md section 8).
-template <int MT, int NS, int K0, int RA, bool TAPE, int WPB = 4, int OCC = 1, bool PAIR = false>
+// GEN: the general white-noise model (per-backend efac / equad, ECORR epoch columns in the
+// hyper block, up to 8 parameters; gibbs.py:64-77) -- one chain per SIMD, no pair mode.
+template <int MT, int NS, int K0, int RA, bool TAPE, int WPB = 4, int OCC = 1, bool PAIR = false,
+          bool GEN = false>
 __global__ void __launch_bounds__(64 * WPB, OCC)
     gst_sweep_kernel(const DevModel* __restrict__ mds, const DevState st, const DevRec rec, const DevTape tape,
                      int C, int nsweeps, long long sweep0, int record_every, unsigned mask,
                      unsigned long long seed, long long chain0, int eval_only, double* out_w,
                      double* out_h) {
   static_assert(!PAIR || (WPB == 2 && !TAPE), "pair mode: one chain per 2-wave workgroup");
+  static_assert(!GEN || (!PAIR && OCC == 1), "general white noise: one chain per wave and SIMD");
+  constexpr int PX = GEN ? 8 : 4;     // parameters held in registers
   constexpr int NSL = SL(MT, 0);
   constexpr int NT = MT / 2;          // 16-wide MFMA tiles
   constexpr int NTT = NT * (NT + 1) / 2;
@@ -1048,9 +1079,9 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   rng.sweep = 0;
 
   // ---------------- load chain state ----------------
-  double xv[4] = {0.0, 0.0, 0.0, 0.0};
+  double xv[PX] = {};
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < PX; ++j)
     if (j < P) xv[j] = xrow[j];
   double theta = st.theta[c];
   double nu = st.nu[c];
@@ -1140,11 +1171,11 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   // one-wave-per-SIMD builds (registers to spare): the prior bounds and efac choice held in
   // registers for the launch instead of re-read from the model descriptor at every call
   // (no machine LICM in this build: each read was a load and a wait)
-  double hpmin[4], hpmax[4], hlp = 0.0, hefc = 1.0;
+  double hpmin[PX], hpmax[PX], hlp = 0.0, hefc = 1.0;
   int hief = -1;
   if constexpr (OCC == 1) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < PX; ++j) {
       hpmin[j] = j < P ? md.pmin[j] : 0.0;
       hpmax[j] = j < P ? md.pmax[j] : 0.0;
     }
@@ -1152,10 +1183,10 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     hief = md.idx_efac;
     hefc = md.efac_const;
   }
-  auto lnprior = [&](const double (&xq)[4]) __attribute__((always_inline)) -> double {
+  auto lnprior = [&](const double (&xq)[PX]) __attribute__((always_inline)) -> double {
     bool in = true;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < PX; ++j) {
       if (OCC == 1) {
         if (j < P) in = in && (xq[j] >= hpmin[j]) && (xq[j] <= hpmax[j]);
       } else {
@@ -1165,10 +1196,36 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     return in ? (OCC == 1 ? hlp : md.lp_sum) : -INFINITY;
   };
 
-  auto efac2_of = [&](const double (&xq)[4]) __attribute__((always_inline)) -> double {
+  auto efac2_of = [&](const double (&xq)[PX]) __attribute__((always_inline)) -> double {
     const double ef = OCC == 1 ? (hief >= 0 ? pget(xq, hief) : hefc)
                                : (md.idx_efac >= 0 ? pget(xq, md.idx_efac) : md.efac_const);
     return ef * ef;
+  };
+
+  // GEN: N0 = efac_b^2 sigma^2 + 10^(2 equad_b) of the TOA's backend b (gibbs.py:262-284 with
+  // the enterprise white-noise signal per backend).  The parameter indices of each of the
+  // lane's TOA slots and of its noise class (lane u < ncls) are held for the launch.
+  int gef[GEN ? NS : 1], geq[GEN ? NS : 1], gcef = -1, gceq = 0;
+  if constexpr (GEN) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int b = ((vmask >> s) & 1u) && md.bk ? md.bk[64 * s + lane] : 0;
+      gef[s] = md.efac_b[b];
+      geq[s] = md.equad_b[b];
+    }
+    const int cb = lane < md.ncls ? md.cls_b[lane] : 0;
+    gcef = md.efac_b[cb];
+    gceq = md.equad_b[cb];
+  }
+  auto gen_n0 = [&](const double (&xq)[PX], double s2, int ie, int iq)
+      __attribute__((always_inline)) -> double {
+    const double ef = ie >= 0 ? pget(xq, ie) : md.efac_const;
+    return ef * ef * s2 + exp(2.0 * pget(xq, iq) * 2.302585092994045684);
+  };
+  // N0 of noise class k (wave-uniform k)
+  auto cls_n0 = [&](const double (&xq)[PX], int k) __attribute__((always_inline)) -> double {
+    const int b = md.cls_b[k];
+    return gen_n0(xq, md.csig2[k], md.efac_b[b], md.equad_b[b]);
   };
 
   // white-noise conditional likelihood (gibbs.py:262-284).  Class path: TOAs with equal
@@ -1201,16 +1258,20 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     }
   };
   // Q = 10^(2 equad) is passed in: the MH steps carry it (Q_q = Q_x * 10^(2 delta)).
-  auto lnl_white = [&](const double (&xq)[4], double Q) __attribute__((always_inline)) -> double {
+  auto lnl_white = [&](const double (&xq)[PX], double Q) __attribute__((always_inline)) -> double {
     const double ef2 = efac2_of(xq);
-    if (hncls == 1) {  // uniform: no reduction
+    if (GEN && hncls == 1) {
+      const double N0 = cls_n0(xq, 0);
+      return -0.5 * ((wcls_la + md.ccount[0] * log(N0)) + rdlane(wcls, 0) / N0);
+    }
+    if (!GEN && hncls == 1) {  // uniform: no reduction
       const double N0 = ef2 * md.csig2[0] + Q;
       return -0.5 * ((wcls_la + md.ccount[0] * log(N0)) + rdlane(wcls, 0) / N0);
     }
     double sl = 0.0, sq = 0.0;
     if (hncls > 1) {
       if (lane < md.ncls) {
-        const double N0 = ef2 * md.csig2[lane] + Q;
+        const double N0 = GEN ? gen_n0(xq, md.csig2[lane], gcef, gceq) : ef2 * md.csig2[lane] + Q;
         sl = md.ccount[lane] * log(N0);
         sq = wcls / N0;
       }
@@ -1222,7 +1283,11 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       if (vmask & (1u << s)) {
-        const double N0 = ef2 * S2(s) + Q;
+        double N0;
+        if constexpr (GEN)
+          N0 = gen_n0(xq, S2(s), gef[s], geq[s]);
+        else
+          N0 = ef2 * S2(s) + Q;
         const double N = ((zb >> s) & 1u ? al[s] : 1.0) * N0;
         lp.mul(N);
         sq += div_pos(yv[s] * yv[s], N);
@@ -1258,7 +1323,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         rng.uniform2(0u, tag | (uint32_t)(3 * step + 2), uidx, unused);
         int k = (int)(uidx * nind);
         k = k < nind - 1 ? k : nind - 1;
-        par = (double)(white ? iget4(md.wind, k) : iget4(md.hind, k));
+        par = (double)(white ? iget<PX>(md.wind, k) : iget<PX>(md.hind, k));
       }
       int cnt = 0;
 #pragma unroll
@@ -1279,14 +1344,14 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
 
   // MH proposal of global step gs (gibbs.py:90-97 / 123-130): q = x with q[par] += delta;
   // returns log(u_accept).  E receives 10^(2 delta) (equad moves rescale Q by it).
-  auto propose = [&](const double (&xq)[4], double (&qv)[4], int gs, double& E, int& par)
+  auto propose = [&](const double (&xq)[PX], double (&qv)[PX], int gs, double& E, int& par)
       __attribute__((always_inline)) -> double {
     const double* e = gs < NWHITE ? mhw + 4 * gs : mhh + 4 * (gs - NWHITE);
     par = (int)e[0];
     const double delta = e[1];
     E = e[3];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) qv[j] = (j == par) ? xq[j] + delta : xq[j];
+    for (int j = 0; j < PX; ++j) qv[j] = (j == par) ? xq[j] + delta : xq[j];
     return e[2];
   };
 
@@ -1300,7 +1365,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   // SVD noise floor f of this sweep's b draw (floor_shift; 0 except on the floor redo)
   double fshift = 0.0;
   // Gram: G = T_aug^T diag(1/N) T_aug on fp64 MFMA, then TM elimination -> S0.
-  auto gram_and_tm = [&](const double (&xq)[4]) __attribute__((always_inline)) {
+  auto gram_and_tm = [&](const double (&xq)[PX]) __attribute__((always_inline)) {
     const double ef2 = efac2_of(xq);
     const double Q = exp(2.0 * pget(xq, md.idx_equad) * 2.302585092994045684);
     double sr = 0.0;
@@ -1310,7 +1375,12 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       const int t = 64 * s + lane;
       double w = 0.0;
       if (vmask & (1u << s)) {
-        const double N = ((zb >> s) & 1u ? al[s] : 1.0) * (ef2 * S2(s) + Q);
+        double N0;
+        if constexpr (GEN)
+          N0 = gen_n0(xq, S2(s), gef[s], geq[s]);
+        else
+          N0 = ef2 * S2(s) + Q;
+        const double N = ((zb >> s) & 1u ? al[s] : 1.0) * N0;
         lp.mul(N);
         const double rs = RR(s);
         sr += rs * rs / N;
@@ -1336,7 +1406,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       for (int i = 0; i < SL(MT, 0); ++i) L[i] = 0.0;
 #pragma unroll 1
       for (int k = 0; k < md.ncls; ++k) {
-        const double ck = 1.0 / (ef2 * md.csig2[k] + Q);
+        const double ck = 1.0 / (GEN ? cls_n0(xq, k) : ef2 * md.csig2[k] + Q);
         const GDouble* gk = (const GDouble*)md.Gcls + (size_t)k * SL(MT, 0) * 64 + lane;
 #pragma unroll
         for (int i = 0; i < SL(MT, 0); ++i) L[i] = fma(ck, gk[64 * i], L[i]);
@@ -1351,7 +1421,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
           const int t = 64 * s + __builtin_ctzll(bm);
           bm &= bm - 1;
           const int k = md.ncls > 1 ? md.cidx[t] : 0;
-          const double v = vbuf[t] - 1.0 / (ef2 * md.csig2[k] + Q);
+          const double v = vbuf[t] - 1.0 / (GEN ? cls_n0(xq, k) : ef2 * md.csig2[k] + Q);
           // [T|r]_t at internal columns 8 r + p (row side) and 8 r + q (column side): each
           // lane's MT entries are contiguous in Trow ([t][i % 8][i / 8]), 128-bit loads
           typedef double v2_t __attribute__((ext_vector_type(2)));
@@ -1594,6 +1664,13 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   const bool f_live = lane < RA - md.ntm_pad && lane < md.nf;
   const double lfreq_l = f_live ? md.lfreq[lane] : 0.0;
   const double ldf_l = f_live ? md.ldf[lane] : 0.0;
+  // GEN: the ECORR epoch columns follow the Fourier block (lanes nf .. nf + nec - 1); the
+  // lane's ecorr parameter index, or -1
+  int geci = -1;
+  if constexpr (GEN) {
+    const int e = lane - md.nf;
+    if (e >= 0 && e < md.nec && lane < RA - md.ntm_pad) geci = md.ecorr_b[md.ecb[e]];
+  }
 
   // b-marginalised likelihood at xq (gibbs.py:288-329); factor left in L.
   // the descriptor scalars of lnl_hyper, read once for the launch (wave-uniform: scalar
@@ -1601,7 +1678,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   const int hidxA = md.idx_logA, hidxg = md.idx_gamma, hntmp = md.ntm_pad, hnf = md.nf;
   const double hl12 = md.log_12pi2, hlfyr = md.log_fyr, hslf = md.sum_lfreq,
                hsldf = md.sum_ldf, hldtm = md.logdet_phi_tm;
-  auto lnl_hyper = [&](const double (&xq)[4], int& failed) __attribute__((always_inline)) -> double {
+  auto lnl_hyper = [&](const double (&xq)[PX], int& failed) __attribute__((always_inline)) -> double {
     GST_COUNT(16)
     GST_SUB_BEGIN
     const double lA = pget(xq, hidxA);
@@ -1615,13 +1692,26 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       for (int s = K0; s <= r; ++s) L[SL(r, s)] = S0[64 * SL(r - K0, s - K0)];
     // Fourier columns, then the unit-prior dummies that pad a smaller model up to this
     // instance's RA (zero Gram rows: each is eliminated as an exact no-op)
-    if (lane < RA - hntmp)
-      phbuf[hntmp + lane] = f_live ? exp(-(lc - g * lfreq_l + ldf_l)) + fshift : 1.0;
+    if constexpr (GEN) {
+      // ECORR column of backend b: phi = 10^(2 ecorr_b) (as the large path, gst_large.hpp)
+      if (lane < RA - hntmp)
+        phbuf[hntmp + lane] =
+            f_live ? exp(-(lc - g * lfreq_l + ldf_l)) + fshift
+                   : (geci >= 0 ? exp(-2.0 * pget(xq, geci) * 2.302585092994045684) + fshift : 1.0);
+    } else {
+      if (lane < RA - hntmp)
+        phbuf[hntmp + lane] = f_live ? exp(-(lc - g * lfreq_l + ldf_l)) + fshift : 1.0;
+    }
     // phbuf doubles as the eliminations' junk rows: restore the one other entry read
     // below, the augmented row's (no prior on the residual column)
     if (lane == 63) phbuf[raug] = 0.0;
     // sum_k log phi_k in closed form (no reduction on the critical path)
-    const double logdet_phi = ((double)hnf * lc - g * hslf + hsldf) + hldtm;
+    double logdet_phi = ((double)hnf * lc - g * hslf + hsldf) + hldtm;
+    if constexpr (GEN) {
+      for (int b = 0; b < md.nb; ++b)   // log 10^(2 ecorr_b) per ECORR column of backend b
+        if (md.ec_count[b] > 0.0)
+          logdet_phi += md.ec_count[b] * (2.0 * pget(xq, md.ecorr_b[b]) * 2.302585092994045684);
+    }
     lds_order();
 #pragma unroll
     for (int r = K0; r < MT; ++r)
@@ -1718,7 +1808,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     GST_STAMP(0)
 
     // ---- white-noise MH block (gibbs.py:114-143); step -1 = the initial lnlike0
-    if ((mask & 1u) && !eval_only && md.ncls > 0) {
+    if ((mask & 1u) && !eval_only && !GEN && md.ncls > 0) {
       // Noise-class path: a likelihood is a few scalar ops (no TOA reduction), so the
       // block is a serial chain of log/divide latencies.  Evaluate it speculatively:
       // for the next D steps, lane 2^j - 1 + b evaluates step s0+j's proposal on the
@@ -1732,7 +1822,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       double Wu[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) Wu[u] = (u < md.ncls) ? rdlane(wcls, u) : 0.0;
-      auto lnl_lane = [&](const double (&xq)[4], double Q) __attribute__((always_inline)) -> double {
+      auto lnl_lane = [&](const double (&xq)[PX], double Q) __attribute__((always_inline)) -> double {
         const double ef2 = efac2_of(xq);
         if (md.ncls == 1) {
           const double N0 = ef2 * md.csig2[0] + Q;
@@ -1773,14 +1863,14 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
           lu[i] = mhw[4 * gs + 2];
           ev[i] = mhw[4 * gs + 3];
         }
-        double xq[4], Q = Qx;
+        double xq[PX], Q = Qx;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) xq[t] = xv[t];
+        for (int t = 0; t < PX; ++t) xq[t] = xv[t];
 #pragma unroll
         for (int i = 0; i < D - 1; ++i) {
           const bool on = i < j && ((b >> i) & 1);
 #pragma unroll
-          for (int t = 0; t < 4; ++t) xq[t] = (on && t == pr[i]) ? xq[t] + dl[i] : xq[t];
+          for (int t = 0; t < PX; ++t) xq[t] = (on && t == pr[i]) ? xq[t] + dl[i] : xq[t];
           Q = (on && pr[i] == ieq) ? Q * ev[i] : Q;
         }
         // the proposal of step s0 + j from the node's state (propose(): q[par] += delta)
@@ -1792,9 +1882,9 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
           delta = j == i ? dl[i] : delta;
           E = j == i ? ev[i] : E;
         }
-        double qv[4];
+        double qv[PX];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) qv[t] = (t == par) ? xq[t] + delta : xq[t];
+        for (int t = 0; t < PX; ++t) qv[t] = (t == par) ? xq[t] + delta : xq[t];
         double p1 = -INFINITY, l1 = 0.0;
         if (j < nd) {
           const double Qq = (par == ieq) ? Q * E : Q;
@@ -1822,7 +1912,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         for (int i = 0; i < D; ++i) {
           const bool on = i < nd && ((path >> i) & 1);
 #pragma unroll
-          for (int t = 0; t < 4; ++t) xv[t] = (on && t == pr[i]) ? xv[t] + dl[i] : xv[t];
+          for (int t = 0; t < PX; ++t) xv[t] = (on && t == pr[i]) ? xv[t] + dl[i] : xv[t];
           Qx = (on && pr[i] == ieq) ? Qx * ev[i] : Qx;
         }
       }
@@ -1833,10 +1923,10 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
 #pragma unroll 1
       for (int step = -1; step < NWHITE; ++step) {
         if ((step & 3) == 0) fair_prio<OCC>(fair);
-        double qv[4], luacc = 0.0, Qq = Qx;
+        double qv[PX], luacc = 0.0, Qq = Qx;
         if (step < 0) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) qv[j] = xv[j];
+          for (int j = 0; j < PX; ++j) qv[j] = xv[j];
         } else {
           double E;
           int par;
@@ -1860,7 +1950,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         }
         if ((l1 + p1) - (l0 + p0) > luacc) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) xv[j] = qv[j];
+          for (int j = 0; j < PX; ++j) xv[j] = qv[j];
           l0 = l1;
           p0 = p1;
           Qx = Qq;
@@ -1883,9 +1973,9 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         int j = init ? 0 : NHYPER, rp = 0;
         // first step >= s whose proposal from xb is inside the prior (the others are
         // rejected without a likelihood, gibbs.py:100-104 with lnprior = -inf)
-        auto next_in = [&](const double (&xb)[4], int s) __attribute__((always_inline)) -> int {
+        auto next_in = [&](const double (&xb)[PX], int s) __attribute__((always_inline)) -> int {
           for (; s < NHYPER; ++s) {
-            double qv[4], E;
+            double qv[PX], E;
             int par;
             (void)propose(xb, qv, NWHITE + s, E, par);
             if (lnprior(qv) != -INFINITY) break;
@@ -1895,14 +1985,14 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         // one sequential MH step (gibbs.py:99-110) at step s with the lnL of its point
         auto decide = [&](int s, double l1, bool f1, int who) __attribute__((always_inline)) {
           if (f1) status |= 1;
-          double qv[4], E;
+          double qv[PX], E;
           int par;
           const double luacc = propose(xv, qv, NWHITE + s, E, par);
           const double p1 = lnprior(qv);
           if ((l1 + p1) - (l0 + p0) > luacc) {
             GST_COUNT(18)
 #pragma unroll
-            for (int t = 0; t < 4; ++t) xv[t] = qv[t];
+            for (int t = 0; t < PX; ++t) xv[t] = qv[t];
             l0 = l1;
             p0 = p1;
             owner = who;
@@ -1933,15 +2023,15 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
             if (!(mask & 4u)) break;
             redraw = true;
 #pragma unroll
-            for (int t = 0; t < 4; ++t)
+            for (int t = 0; t < PX; ++t)
               if (t < P) redraw = redraw && (xv[t] != x_last0);      // gibbs.py:373
             if (mask & 128u) redraw = true;
             if (!redraw || owner >= 0) break;
             fin = true;
           }
-          double qa[4];
+          double qa[PX];
 #pragma unroll
-          for (int t = 0; t < 4; ++t) qa[t] = xv[t];
+          for (int t = 0; t < PX; ++t) qa[t] = xv[t];
           int kind = 0, sb = NHYPER;   // wave 1: 0 idle, 1 accept branch, 2 reject branch, 3 x
           if (!fin) {
             if (!init) {
@@ -1961,9 +2051,9 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
               kind = 3;
             }
           }
-          double xq[4];
+          double xq[PX];
 #pragma unroll
-          for (int t = 0; t < 4; ++t) xq[t] = role == 0 ? qa[t] : xv[t];
+          for (int t = 0; t < PX; ++t) xq[t] = role == 0 ? qa[t] : xv[t];
           if (role == 1 && (kind == 1 || kind == 2)) {
             double E;
             int par;
@@ -2019,7 +2109,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         if (pass == 1 || !redraw || fb || (st.debug & DEBUG_EXACT_BDRAW)) break;
         // the owner wave holds the factor at the final x; both waves take its floor decision
         const double fs =
-            role == owner ? floor_shift(f_apr, lane, md.ntm, md.ntm_pad, md.ntm_pad + md.nf) : 0.0;
+            role == owner ? floor_shift(f_apr, lane, md.ntm, md.ntm_pad, md.ntm_pad + md.nf + (GEN ? md.nec : 0)) : 0.0;
         if (role == owner && lane == 0) xfloor[0] = fs;
         __syncthreads();
         fshift = xfloor[0];
@@ -2050,19 +2140,19 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
 #pragma unroll 1
       for (int step = pass ? NHYPER : first; step <= NHYPER; ++step) {
         fair_prio<OCC>(fair);
-        double qv[4], luacc = 0.0;
+        double qv[PX], luacc = 0.0;
         if (step == NHYPER) {
           if (eval_only || !(mask & 4u)) break;
           redraw = true;
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < PX; ++j)
             if (j < P) redraw = redraw && (xv[j] != x_last0);   // gibbs.py:373
           if (mask & 128u) redraw = true;                        // direct update_b call
           if (!redraw || Lvalid) break;
         }
         if (step < 0 || step == NHYPER) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) qv[j] = xv[j];
+          for (int j = 0; j < PX; ++j) qv[j] = xv[j];
         } else {
           double E;
           int par;
@@ -2092,7 +2182,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         if ((l1 + p1) - (l0 + p0) > luacc) {
           GST_COUNT(18)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) xv[j] = qv[j];
+          for (int j = 0; j < PX; ++j) xv[j] = qv[j];
           l0 = l1;
           p0 = p1;
           Lvalid = true;
@@ -2101,7 +2191,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         }
       }
       if (pass == 1 || eval_only || !redraw || fb || (st.debug & DEBUG_EXACT_BDRAW)) break;
-      fshift = floor_shift(f_apr, lane, md.ntm, md.ntm_pad, md.ntm_pad + md.nf);
+      fshift = floor_shift(f_apr, lane, md.ntm, md.ntm_pad, md.ntm_pad + md.nf + (GEN ? md.nec : 0));
       if (__builtin_expect(fshift == 0.0, 1)) break;
       status |= STATUS_FLOOR;
       ++nfloor;
@@ -2284,7 +2374,11 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       for (int s = 0; s < NS; ++s) {
         if (mine & (1u << s)) {
           const int t = 64 * s + lane;
-          const double N0 = ef2 * S2(s) + Q;
+          double N0;
+          if constexpr (GEN)
+            N0 = gen_n0(xv, S2(s), gef[s], geq[s]);
+          else
+            N0 = ef2 * S2(s) + Q;
           const double Nv = al[s] * N0;
           const double y = yv[s];
           const double sd1 = sqrt(Nv);
@@ -2355,7 +2449,11 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         for (int s = 0; s < NS; ++s) {
           if (mine & (1u << s)) {
             const double zf = (double)((zb >> s) & 1u);
-            const double N0 = ef2 * S2(s) + Q;
+            double N0;
+            if constexpr (GEN)
+              N0 = gen_n0(xv, S2(s), gef[s], geq[s]);
+            else
+              N0 = ef2 * S2(s) + Q;
             const double top = ((yv[s] * yv[s]) * zf / N0 + nu) / 2.0;
             al[s] = top / G[s];
           }

@@ -201,7 +201,7 @@ def scaled_synthetic(n: int = 100_000, components: int = 60, ntm: int = 300, see
 def multiband(nepochs: int = 60, nsub: int = 3, backends=("ASP", "GUPPI"), seed: int = 1643,
               theta: float = 0.05, sigma_out: float = 1e-6, efac=(1.1, 0.9),
               log10_equad=(-6.6, -7.0), log10_ecorr=(-6.5, -6.8), log10_A: float = -14.0,
-              gamma: float = 4.33, components: int = 10) -> PulsarData:
+              gamma: float = 4.33, components: int = 10, nerr: int = 0) -> PulsarData:
     """A NANOGrav-style multi-backend, multi-band dataset for the general white-noise model
     of the notebook's J1643-1224 run (gibbs_likelihood.ipynb cell 2: efac, equad, ECORR per
     backend, power-law red noise, timing model) -- not in the reference's data, built with
@@ -211,7 +211,9 @@ def multiband(nepochs: int = 60, nsub: int = 3, backends=("ASP", "GUPPI"), seed:
     epoch), the first half of the epochs on ``backends[0]``, the rest on ``backends[1]``;
     white noise ``efac_b sigma`` + ``10^equad_b`` per TOA, ECORR jitter ``10^ecorr_b`` shared
     by an epoch's TOAs, power-law red noise, Bernoulli(theta) outliers, and the timing model
-    projected out.  The per-backend true values are in ``meta``."""
+    projected out.  The per-backend true values are in ``meta``.  ``nerr`` > 0: every TOA's
+    error bar is one of ``nerr`` values (a few noise classes per backend, as a receiver's
+    quantised template-fit errors give) instead of log-normal."""
     raw = load_j1713_raw()
     mjd0 = (raw["mjd_int"].astype(np.float64) + raw["mjd_frac"])[:nepochs]
     rng = np.random.default_rng(seed)
@@ -222,6 +224,8 @@ def multiband(nepochs: int = 60, nsub: int = 3, backends=("ASP", "GUPPI"), seed:
     bk = (ep >= nepochs // 2).astype(np.int64)
     labels = np.array(backends)[bk]
     err = 10 ** (-7 + rng.standard_normal(n) * 0.2)
+    if nerr > 0:
+        err = 10 ** (-7 + 0.2 * (rng.integers(0, nerr, size=n) - (nerr - 1) / 2.0))
     M = design_matrix(mjd, raw["par"], raw["fit"])
     U = np.linalg.svd(M, full_matrices=False)[0]
     F, ff = fourier_basis(toas, components)

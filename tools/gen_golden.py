@@ -436,6 +436,25 @@ def small_ecorr(niter=12):
                   np.nanmax(out["tape_b_cond"]), file=sys.stderr)
 
 
+def ecorr_classes(niter=12):
+    """``ecq``: the ``ecb`` model (per-backend efac / equad / ECORR, 20 Fourier + 24 ECORR
+    columns) on a pulsar whose error bars take two values (gdata.multiband nerr = 2): four
+    noise classes (error bar x backend), so the persistent kernel's general white-noise
+    instances take their noise-class likelihood and low-rank Gram paths (gst_kernel.hpp
+    lnl_white / gram_and_tm with GEN)."""
+    psr = gdata.multiband(nepochs=24, nsub=3, seed=2445, nerr=2)
+    pta_q = PTA(psr, components=10, efac=(0.2, 10.0), selection="backend",
+                log10_ecorr=(-8.5, -5.0))
+    x0 = [1.1, -6.5, -6.6, 0.9, -6.8, -7.0, 4.33, -14.0]
+    np.savez_compressed(os.path.join(OUTDIR, "ecq_dataset.npz"), **dataset_arrays(pta_q, psr))
+    for j, name in enumerate(("beta", "t")):
+        out = run_one(pta_q, name, MODELS[name], seed=7900 + 13 * j, niter=niter, x0=x0)
+        out["model_kw"] = np.array(repr(MODELS[name]))
+        np.savez_compressed(os.path.join(OUTDIR, f"ref_ecq_{name}_fixed.npz"), **out)
+        print("ecq", name, "P", len(x0), "m", pta_q.m, "cond:",
+              np.nanmax(out["tape_b_cond"]), file=sys.stderr)
+
+
 def mid(niter=12):
     """A mid-size pulsar for the register-resident kernel's wide TOA instances (NS = 6, 8
     slots of 64 TOAs): 130 J1713+0747 epochs x 3 sub-band TOAs (gdata.multiband, one
@@ -477,6 +496,9 @@ def main():
         return
     if "--only-small-ecorr" in sys.argv:
         small_ecorr(12)
+        return
+    if "--only-ecorr-classes" in sys.argv:
+        ecorr_classes(12)
         return
     if "--only-mid" in sys.argv:
         mid(12)
@@ -539,6 +561,8 @@ def main():
     configs34(niter)
     shapes(niter)
     general(niter)
+    small_ecorr(niter)
+    ecorr_classes(niter)
     mid(niter)
     wide(niter)
 
