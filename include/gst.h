@@ -214,7 +214,9 @@ int gst_sync(void* ctx, void* stream);
 /* Execution path.  The persistent path keeps a whole chain in one wavefront for all of a
  * launch's sweeps (n <= 512 and up to 30 red-noise components with <= 16 timing-model
  * columns, 26 with <= 24, n <= 1024 for the 30-component / 16-column shape; smaller models
- * run padded with unit-prior dummy columns); the
+ * run padded with unit-prior dummy columns; the general white-noise model -- per-backend
+ * efac / equad, ECORR columns, up to 8 parameters -- with <= 16 timing-model columns, up to
+ * 60 Fourier + ECORR columns and n <= 512, one chain per SIMD); the
  * large path runs
  * each sweep as a pipeline of kernels (fp64-MFMA Gram shared by all chains, blocked
  * timing-model elimination, LDS-resident red-noise MH, MFMA T b, per-TOA passes) for
@@ -229,7 +231,8 @@ int gst_get_path(void* ctx, int* path);
  * that split the red-noise MH block's likelihood evaluations (AUTO, the default); the
  * chain's draws are bitwise those of the one-wave kernel.  GST_WAVES_ONE / GST_WAVES_TWO
  * force either kernel for every sampling launch (tape-mode and gst_eval_lnlike launches
- * always run one wave per chain). */
+ * always run one wave per chain).  The general white-noise model has no two-wave kernel: AUTO
+ * runs it on one wave, and a sweep with GST_WAVES_TWO set fails. */
 enum gst_waves { GST_WAVES_AUTO = 0, GST_WAVES_ONE = 1, GST_WAVES_TWO = 2 };
 int gst_set_waves(void* ctx, int waves);
 
