@@ -33,7 +33,7 @@ def rate(pta, C, S, path):
         ns.sweep(S, seed=1, sweep0=20 + S)
         ns.synchronize()
         ms = sum(v[0] for v in ns.kernel_times().values())
-    ok = bool(np.all(ns.get_state()["status"] == 0))
+    ok = bool(np.all((ns.get_state()["status"] & 0xef) == 0))   # floor draws are not errors
     ns.close()
     return C * S / (ms * 1e-3), ms / S, ok
 
@@ -43,10 +43,15 @@ def main():
     S = int(sys.argv[2]) if len(sys.argv) > 2 else 100
     out = {"chains": C, "sweeps": S, "model": "run_sims 'beta', 30 components, 14 TM columns",
            "rows": []}
-    for nepochs, nsub in ((130, 2), (130, 3), (128, 4), (130, 5), (130, 7)):
+    # MS_SIZES: sub-band TOAs per J1713 epoch (130 epochs; 128 x 4 = 512); MS_PATHS: the paths
+    import os
+    sizes = [int(v) for v in os.environ.get("MS_SIZES", "2,3,4,5,7").split(",")]
+    paths = os.environ.get("MS_PATHS", "persistent,large").split(",")
+    for nsub in sizes:
+        nepochs = 128 if nsub == 4 else 130
         psr = data.multiband(nepochs=nepochs, nsub=nsub, seed=7)
         pta = PTA(psr)
-        for path in ("persistent", "large"):
+        for path in paths:
             r, ms, ok = rate(pta, C, S if path == "persistent" else max(2, S // 10), path)
             row = {"n": pta.n, "path": path, "chain_sweeps_per_s": r, "ms_per_sweep": ms,
                    "status_clean": ok}
