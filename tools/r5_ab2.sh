@@ -1,14 +1,15 @@
 #!/bin/bash
 # Interleaved A/B of named variants: NAME=ENV... pairs, e.g.
 #   tools/r5_ab2.sh 3 base:GST_LIB=gibbs_student_t_amd/libgst.so tb16:GST_LIB=gibbs_student_t_amd/libgst_tb16.so
-# config 2 at 500 and 20 sweeps, config 3 at 500 sweeps per variant and round.
+# config 2 at 500 and 20 sweeps, config 3 at 500 sweeps per variant and round (AB_C4=1: and
+# config 4 at 100 sweeps).
 set -o pipefail
 R=$1; shift
 O=gpurun_out/ab52; mkdir -p $O
 for r in $(seq 1 $R); do
 for v in "$@"; do
   n=${v%%:*}; envs=${v#*:}
-  for a in "--steps 500 --warmup 50" "--steps 20 --warmup 5" "--config 3 --steps 500 --warmup 50"; do
+  for a in "--steps 500 --warmup 50" "--steps 20 --warmup 5" "--config 3 --steps 500 --warmup 50" ${AB_C4:+"--config 4 --steps 100 --warmup 20"}; do
     tag=$(echo "$a" | tr -d ' -')
     env ${envs//,/ } timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-stage-costs --ess-window 0 $a \
       > $O/$n.$tag.$r.json 2> $O/$n.$tag.$r.err || { echo "FAIL $n $a"; tail -3 $O/$n.$tag.$r.err; exit 1; }
