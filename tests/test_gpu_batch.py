@@ -230,3 +230,44 @@ def test_large_path_chains_do_not_depend_on_batch_partners():
             for k in ("z", "alpha", "pout"):
                 np.testing.assert_array_equal(full[k][sl][:, :n], ref[k][:, :n],
                                               err_msg=f"{members} {d} {k}")
+
+
+def test_general_white_noise_batch_matches_single_datasets():
+    """The persistent kernel's general white-noise instances (per-backend efac / equad, ECORR;
+    DESIGN.md 4d) in a batch of two structurally equal datasets -- ``ecb`` (every TOA its own
+    error bar: per-TOA likelihood, MFMA Gram) and ``ecq`` (four noise classes: class
+    likelihood, low-rank Gram) -- give each dataset's chains bitwise as when it runs alone:
+    every per-dataset table (TOA backends, ECORR column backends, noise classes and their
+    backends, class Grams) is read from the chain's own dataset."""
+    refs = [load_ref("ecb_beta_fixed"), load_ref("ecq_beta_fixed")]
+    per, S, seed = 24, 6, 9
+
+    def init(ref, c0):
+        pta = ref["pta"]
+        lo = np.array([p.pmin for p in pta.params])
+        hi = np.array([p.pmax for p in pta.params])
+        s0 = sweep_state(ref, 0)
+        return dict(x=np.stack([np.random.default_rng([11, c0 + c]).uniform(lo, hi)
+                                for c in range(per)]),
+                    b=np.tile(s0["b"], (per, 1)), z=np.tile(s0["z"], (per, 1)),
+                    alpha=np.tile(s0["alpha"], (per, 1)), pout=np.tile(s0["pout"], (per, 1)),
+                    theta=np.full(per, s0["theta"]), nu=np.full(per, s0["nu"]))
+
+    big = NativeSampler([r["pta"] for r in refs], [r["kw"] for r in refs], 0, path="persistent")
+    big.alloc(2 * per, dataset=np.repeat(np.arange(2), per))
+    parts = [init(r, j * per) for j, r in enumerate(refs)]
+    big.set_state(**{k: np.concatenate([p[k] for p in parts]) for k in parts[0]})
+    big.sweep(S, seed=seed, sweep0=3)
+    full = big.get_state()
+    big.close()
+    assert np.all((full["status"] & STATUS_ERRORS) == 0)
+    for j, ref in enumerate(refs):
+        one = NativeSampler(ref["pta"], ref["kw"], 0, path="persistent")
+        one.alloc(per)
+        one.set_state(**parts[j])
+        one.sweep(S, seed=seed, sweep0=3, chain0=j * per)
+        alone = one.get_state()
+        one.close()
+        sl = slice(j * per, (j + 1) * per)
+        for k in ("x", "b", "z", "alpha", "pout", "theta", "nu", "status"):
+            np.testing.assert_array_equal(full[k][sl], alone[k], err_msg=f"dataset {j} {k}")
