@@ -54,6 +54,19 @@ def test_general_white_noise_path_choice(name):
     ref = load_ref(name)
     ns = NativeSampler(ref["pta"], ref["kw"], 0)
     assert ns.path == ("persistent" if name.startswith("ec") else "large")
+    if ns.path == "persistent":
+        # no two-waves-per-chain build for these models: asking for it fails loudly
+        ns.alloc(8)
+        s0 = sweep_state(ref, 0)
+        ns.set_state(x=np.tile(ref["chain"][0], (8, 1)), b=np.tile(s0["b"], (8, 1)),
+                     z=np.tile(s0["z"], (8, 1)), alpha=np.tile(s0["alpha"], (8, 1)),
+                     pout=np.tile(s0["pout"], (8, 1)), theta=np.full(8, s0["theta"]),
+                     nu=np.full(8, s0["nu"]))
+        ns.set_waves(2)
+        with pytest.raises(_abi.GstNativeError, match="two waves per chain"):
+            ns.sweep(1, seed=1)
+        ns.set_waves("auto")
+        ns.sweep(1, seed=1)
     ns.close()
 
 
