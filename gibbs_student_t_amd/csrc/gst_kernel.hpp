@@ -166,7 +166,7 @@ constexpr int TP_WHITE = 0, TP_HYPER = 80, TP_DELTA = 120;
 // the 8 p-rows of a 128-bit read in distinct bank groups (80 B apart).
 
 // diagnostic builds: slots 0-15, 19-23 cycle sums (tools/stage_profile.py), 16-18 event counts
-constexpr int GST_NSTAMP = 24;
+constexpr int GST_NSTAMP = 28;
 #ifdef GST_STAMPS
 #define GST_STAMP_DECL \
   unsigned long long st_acc[GST_NSTAMP] = {0}, st_t0 = 0, st_s0 = 0;
@@ -2348,6 +2348,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
 
     GST_STAMP(4)
     fair_prio<OCC>(fair);
+    GST_SUB_BEGIN
     // ---- outlier block: theta (gibbs.py:185-198)
     const double ef2 = efac2_of(xv);
     const double Q = exp(2.0 * pget(xv, md.idx_equad) * 2.302585092994045684);
@@ -2368,6 +2369,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       }
     }
     fair_prio<OCC>(fair);
+    GST_SUB_END(23)
     // ---- z (gibbs.py:201-226)
     // pair mode: each wave draws z and alpha for its half of the TOA slots (Philox is keyed
     // by TOA, so every draw is the one the single-wave kernel makes) and takes the other
@@ -2431,6 +2433,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       }
     }
     fair_prio<OCC>(fair);
+    GST_SUB_END(24)
     // ---- alpha (gibbs.py:229-242)
     if ((mask & 32u) && md.vary_alpha) {
       int zs = 0;
@@ -2475,6 +2478,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
         }
       }
     }
+    GST_SUB_END(25)
     GST_STAMP(5)
     // ---- nu (gibbs.py:244-259, 331-335)
     if ((mask & 64u) && md.vary_df) {

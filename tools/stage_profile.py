@@ -44,7 +44,7 @@ def main():
         ns.set_state(x=x0, z=np.ones((C, ns.n)), alpha=np.ones((C, ns.n)),
                      theta=np.full(C, 0.01), nu=np.full(C, 4.0))
     ns.sweep(300, seed=1)
-    buf = torch.zeros((C, 24), dtype=torch.int64, device=ns.tdev)
+    buf = torch.zeros((C, 28), dtype=torch.int64, device=ns.tdev)
     _abi.check(ns.lib, ns.lib.gst_debug_stamps(ns.ctx, ct.c_void_p(buf.data_ptr())),
                "gst_debug_stamps")
     ns.sweep(S, seed=1, sweep0=300)
@@ -58,7 +58,8 @@ def main():
         print(f"  {nm:22s} {np.median(cyc[:, i]):10.0f} cyc  {np.median(cyc[:, i] / tot) * 100:5.1f} %")
 
     for i, nm in ((19, "(hyper: harvest + stats)"), (20, "(record: MH variates)"),
-                  (21, "(white: class sums)"), (22, "(white: lane lnL tree)")):
+                  (21, "(white: class sums)"), (22, "(white: lane lnL tree)"),
+                  (23, "(outlier: theta)"), (24, "(outlier: z)"), (25, "(outlier: alpha)")):
         print(f"  {nm:22s} {np.median(cyc[:, i]):10.0f} cyc  "
               f"{np.median(cyc[:, i] / tot) * 100:5.1f} %")
     for i, nm in ((16, "red-noise lnL evaluations"), (17, "two-wave rounds"),
