@@ -56,7 +56,8 @@ struct Ctx {
   // large path: scratch sized for scratch_C chains, per-kernel timing events
   gst::LScratch ls{};
   int scratch_C = 0;
-  size_t lds_tm = 0, lds_hyper = 0, lds_btm = 0;
+  size_t lds_tm = 0, lds_hyper = 0, lds_btm = 0, lds_hyper_big = 0;
+  bool hyper_big = false;          // large path: a hyper block past HYPER_LDS_MAX (G3 scratch)
   bool timing = false;
   std::vector<hipEvent_t> evpool;
   std::vector<int> evkind;  // kind of event pair i (events 2i, 2i+1)
@@ -67,7 +68,7 @@ struct Ctx {
 // (hipMallocAsync / hipFreeAsync on the launch's stream): no device synchronisation inside
 // gst_sweep, and a buffer is released only after the work queued before it on that stream.
 void free_scratch(Ctx* cx, hipStream_t st) {
-  for (double* p : {cx->ls.G, cx->ls.G2, cx->ls.y, cx->ls.w, cx->ls.sc, cx->ls.v})
+  for (double* p : {cx->ls.G, cx->ls.G2, cx->ls.y, cx->ls.w, cx->ls.sc, cx->ls.v, cx->ls.G3})
     if (p) (void)hipFreeAsync(p, st);
   cx->ls = gst::LScratch{};
   cx->scratch_C = 0;
@@ -537,10 +538,13 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
     return fail(b);
   }
   if (path == GST_PATH_LARGE) {
-    const int ms = nf + nec + 1;
-    if ((size_t)(ms * (ms + 1) + nf + nec + 2 * ms) * 8 > 160 * 1024)
-      return fail("gst_model_set: large path needs nfourier + n_ecorr <= 138 (LDS-resident "
-                  "red-noise / ECORR block)");
+    // hyper blocks past HYPER_LDS_MAX columns are factored in global memory (lg_hyper<true>),
+    // whose LDS holds a 16-column panel of all mp rows plus three vectors of the block
+    const int ms = nf + nec + 1, mpl = round_up(round_up(ntm > 0 ? ntm : 1, 16) + nf + nec + 1, 16);
+    if (nf + nec > gst::HYPER_LDS_MAX &&
+        (size_t)(mpl * (gst::TM_PW + 1) + gst::TM_PW + nf + nec + 2 * ms) * 8 > 160 * 1024)
+      return fail("gst_model_set: large path: basis too large for the LDS panel of the "
+                  "red-noise / ECORR block elimination");
   }
   free_model(cx);
   // large path: timing-model block padded to whole 16-column MFMA tiles, no dummies
@@ -572,14 +576,21 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
     cx->raug = h.raug;
     cx->lds_tm = (size_t)h.mp * (gst::TM_PW + 1) * 8;
     const int ms = h.nf + h.nec + 1;
-    cx->lds_hyper = (size_t)(ms * (ms + 1) + h.nf + h.nec + 2 * ms) * 8;
+    cx->hyper_big = h.nf + h.nec > gst::HYPER_LDS_MAX;
+    cx->lds_hyper = cx->hyper_big ? 0 : (size_t)(ms * (ms + 1) + h.nf + h.nec + 2 * ms) * 8;
+    cx->lds_hyper_big = (size_t)(h.mp * (gst::TM_PW + 1) + gst::TM_PW + h.nf + h.nec + 2 * ms) * 8;
     cx->lds_btm = (size_t)(3 * h.ntm_pad + h.raug) * 8;
     HIP_OK(hipFuncSetAttribute((const void*)gst::lg_gram,
                                hipFuncAttributeMaxDynamicSharedMemorySize, gst::GRAM_LDS * 8));
     HIP_OK(hipFuncSetAttribute((const void*)gst::lg_tmelim,
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)cx->lds_tm));
-    HIP_OK(hipFuncSetAttribute((const void*)gst::lg_hyper,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)cx->lds_hyper));
+    if (!cx->hyper_big)
+      HIP_OK(hipFuncSetAttribute((const void*)gst::lg_hyper<false>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)cx->lds_hyper));
+    else
+      HIP_OK(hipFuncSetAttribute((const void*)gst::lg_hyper<true>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)cx->lds_hyper_big));
     HIP_OK(hipFuncSetAttribute((const void*)gst::lg_btm,
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)cx->lds_btm));
   }
@@ -649,13 +660,17 @@ static int ensure_scratch(Ctx* cx, int C, hipStream_t st) {
   HIP_OK(hipMemsetAsync(cx->ls.G2, 0, (size_t)C * mp * mp * 8, st));
   HIP_OK(hipMemsetAsync(cx->ls.sc, 0, (size_t)C * 16 * 8, st));
   HIP_OK(hipMemsetAsync(cx->ls.v, 0, (size_t)C * mp * 8, st));
+  if (cx->hyper_big) {   // lg_hyper<true>'s factor of the red-noise / ECORR block
+    HIP_OK(hipMallocAsync((void**)&cx->ls.G3, (size_t)C * mp * mp * 8, st));
+    HIP_OK(hipMemsetAsync(cx->ls.G3, 0, (size_t)C * mp * mp * 8, st));
+  }
   cx->scratch_C = C;
   return 0;
 }
 
 // The red-noise MH block's launches: one per hyper kernel class present (gst_large.hpp
 // hyper_class); a chain of another class returns at once.
-static int launch_hyper(Ctx* cx, gst::LArgs& a, const bool (&hcls)[3], dim3 g8, dim3 b8,
+static int launch_hyper(Ctx* cx, gst::LArgs& a, const bool (&hcls)[4], dim3 g8, dim3 b8,
                         dim3 g16, dim3 b16, dim3 g_chain, dim3 b_chain, hipStream_t st) {
   if (hcls[0]) {
     a.kclass = 8;
@@ -667,7 +682,11 @@ static int launch_hyper(Ctx* cx, gst::LArgs& a, const bool (&hcls)[3], dim3 g8, 
   }
   if (hcls[2]) {
     a.kclass = 0;
-    LG_LAUNCH(GST_K_HYPER, gst::lg_hyper, g_chain, b_chain, cx->lds_hyper);
+    LG_LAUNCH(GST_K_HYPER, gst::lg_hyper<false>, g_chain, b_chain, cx->lds_hyper);
+  }
+  if (hcls[3]) {
+    a.kclass = 1;
+    LG_LAUNCH(GST_K_HYPER, gst::lg_hyper<true>, g_chain, b_chain, cx->lds_hyper_big);
   }
   return 0;
 }
@@ -691,12 +710,13 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
   // of up to HR_COLS (62) / HR_COLS_WIDE (126) columns: one wave per chain, register-resident
   // elimination (lg_hyper_reg<8> / <16>); larger ones: lg_hyper (LDS)
   const int hyper_lds = (cx->debug & GST_DEBUG_LARGE_HYPER) ? 1 : 0;
-  bool wcls[3] = {false, false, false}, tcls[2] = {false, false}, hcls[3] = {false, false, false};
+  bool wcls[3] = {false, false, false}, tcls[2] = {false, false};
+  bool hcls[4] = {false, false, false, false};
   for (const gst::DevModel& hm : cx->hmd) {
     wcls[gst::white_class(hm.npad)] = true;
     tcls[gst::toa_class(hm.npad)] = true;
     const int hc = gst::hyper_class(hm.nf + hm.nec, hyper_lds);
-    hcls[hc == 8 ? 0 : (hc == 16 ? 1 : 2)] = true;
+    hcls[hc == 8 ? 0 : (hc == 16 ? 1 : (hc == 0 ? 2 : 3))] = true;
   }
   a.hyper_lds = hyper_lds;
   const dim3 g_hr8((C + gst::HR<8>::WPB - 1) / gst::HR<8>::WPB), b_hr8(64 * gst::HR<8>::WPB);

@@ -48,15 +48,19 @@ constexpr int TBLK_WAVE_NPAD = 8192;
 // a chain whose dataset is of another class returns at once):
 //   lg_white: 0 = one wave (npad <= TBLK_WAVE_NPAD), 1 = TBLK_SMALL, 2 = TBLK threads;
 //   lg_toa:   0 = TBLK_SMALL, 1 = TBLK threads;
-//   hyper:    8 / 16 = lg_hyper_reg<8 / 16> (hyper block of <= 62 / 126 columns), 0 = lg_hyper.
+//   hyper:    8 / 16 = lg_hyper_reg<8 / 16> (hyper block of <= 62 / 126 columns), 0 = lg_hyper
+//             (LDS-resident block, <= HYPER_LDS_MAX columns), 1 = lg_hyper<true> (larger blocks,
+//             e.g. hundreds of ECORR epochs: blocked elimination in global memory).
 __host__ __device__ constexpr int white_class(int npad) {
   return npad <= TBLK_WAVE_NPAD ? 0 : (npad <= TBLK_SMALL_NPAD ? 1 : 2);
 }
 __host__ __device__ constexpr int toa_class(int npad) { return npad <= TBLK_SMALL_NPAD ? 0 : 1; }
 // hyper class from the dataset's own hyper block nf + nec: lg_hyper_reg<MT> takes up to
 // HR<MT>::RA = 8 MT - 2 columns (62 / 126)
+constexpr int HYPER_LDS_MAX = 138;   // lg_hyper's LDS block: (ms (ms + 1) + 3 ms) doubles < 160 KB
 __host__ __device__ constexpr int hyper_class(int hcols, int force_lds) {
-  return force_lds ? 0 : (hcols <= 8 * 8 - 2 ? 8 : (hcols <= 8 * 16 - 2 ? 16 : 0));
+  return hcols > HYPER_LDS_MAX ? 1
+                               : (force_lds ? 0 : (hcols <= 8 * 8 - 2 ? 8 : (hcols <= 8 * 16 - 2 ? 16 : 0)));
 }
 constexpr int GRAM_WAVES = 8;  // chains per gram workgroup
 constexpr int TM_PW = 16;      // panel width of the timing-model elimination
@@ -69,6 +73,7 @@ struct LScratch {
   double* w;   // [C][npad]  1/N (white scratch: y^2/a during the white block)
   double* sc;  // [C][16]    per-chain scalars (SC_*)
   double* v;   // [C][mp]    b-draw solution (internal order)
+  double* G3;  // [C][mp*mp] lg_hyper<true>'s factor of the hyper block (null unless needed)
 };
 enum : int {
   SC_LOGDETN = 0,
@@ -693,40 +698,38 @@ __global__ void __launch_bounds__(64 * GS_WPB) lg_gram_small(const DevModel* __r
 // ------------------------------------------------------------------------------------
 // Panels of 16 columns: the panel (rows k0..mp) is factored in LDS, written back, then the
 // trailing lower triangle is updated by MFMA: G_ij -= sum_kk P_i,kk P_j,kk / a_kk.
-__global__ void __launch_bounds__(LBLK) lg_tmelim(const DevModel* __restrict__ mds, LArgs a) {
-  const int c = blockIdx.x;
-  const DevModel& md = mds[ds_of(a, c)];
-  double* sc = a.s.sc + (size_t)c * 16;
-  // floor pass: only the chains whose b draw runs at the SVD noise floor, with Sigma + f I
-  const double fsh = a.floor_pass ? sc[SC_FLOOR] : 0.0;
-  if (a.floor_pass && !(fsh > 0.0)) return;
-  extern __shared__ double lsm[];
+// Blocked right-looking LDL^T (raw columns) of columns [k_lo, k_hi) of a symmetric mp x mp
+// matrix (row-major, lower triangle): panels of TM_PW columns factored in LDS (P, [mp][TM_PW+1]),
+// each panel written back raw to Gout, the trailing lower triangle (rows / columns past the
+// panel, up to mp) updated by MFMA tiles.  The first panel and its trailing tiles are read from
+// Gin, every later read is of Gout (Gin stays intact).  diag(gk, v) gives diagonal element gk
+// as its panel is loaded (priors are added there: a trailing update never reads a diagonal
+// before its own panel).  Thread 0 accumulates sum log a_kk, sum a_{zrow,k}^2 / a_kk, the
+// smallest / largest pivot of the columns real(gk) selects and the failure flag.  k_lo and mp
+// are multiples of 16; the last panel may be partial (its columns past k_hi are updated, not
+// eliminated).  trail_all: also update the trailing triangle after the last panel (the
+// timing-model elimination leaves the Schur complement S0 there).
+template <class DiagF, class RealF>
+__device__ void panel_ldl(const double* Gin, double* Gout, int mp, int k_lo, int k_hi, int zrow,
+                          bool trail_all, DiagF diag, RealF real, double* P, double* ainv,
+                          double& ld, double& quad, double& pmin, double& pmax, int& fail) {
   constexpr int PS = TM_PW + 1;        // panel row stride
-  double* P = lsm;                     // [mp][PS]
-  __shared__ double ainv[TM_PW];
-  __shared__ double red[4];
-  const int mp = md.mp, K0 = md.ntm_pad, raug = md.raug;
-  // G stays the Gram (the floor pass re-eliminates it); the factor and S0 go to G2: the
-  // first panel reads G, every later read is of G2
-  const double* Gg = a.s.G + (size_t)c * mp * mp;
-  double* Gc = a.s.G2 + (size_t)c * mp * mp;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  double ld = 0.0, quad = 0.0, pmin = INFINITY, pmax = 0.0;
-  int fail = 0;
-  for (int k0 = 0; k0 < K0; k0 += TM_PW) {
+  for (int k0 = k_lo; k0 < k_hi; k0 += TM_PW) {
     const int R = mp - k0;
-    const double* Gin = k0 == 0 ? Gg : Gc;
-    // load the panel; timing-model prior 1/tm_weight on its diagonal, unit pivots on pads
+    const int pw = k_hi - k0 < TM_PW ? k_hi - k0 : TM_PW;
+    const double* Gsrc = k0 == k_lo ? Gin : Gout;
+    // load the panel
     for (int e = tid; e < R * TM_PW; e += LBLK) {
       const int i = e / TM_PW, kk = e % TM_PW;
       const int gi = k0 + i, gk = k0 + kk;
-      double v = (gi >= gk) ? Gin[(size_t)gi * mp + gk] : 0.0;
-      if (gi == gk) v = (gk < md.ntm) ? (v + md.tm_phiinv) + fsh : 1.0;
+      double v = (gi >= gk) ? Gsrc[(size_t)gi * mp + gk] : 0.0;
+      if (gi == gk && kk < pw) v = diag(gk, v);
       P[i * PS + kk] = v;
     }
     __syncthreads();
-    // factor the panel (columns kk, rows kk..R)
-    for (int kk = 0; kk < TM_PW; ++kk) {
+    // factor the panel (columns kk < pw, rows kk..R)
+    for (int kk = 0; kk < pw; ++kk) {
       const double akk = P[kk * PS + kk];
       const double r = 1.0 / akk;
       for (int e = tid; e < (R - kk - 1) * (TM_PW - kk - 1); e += LBLK) {
@@ -736,73 +739,102 @@ __global__ void __launch_bounds__(LBLK) lg_tmelim(const DevModel* __restrict__ m
       }
       if (tid == 0) {
         fail |= !(akk > 0.0) ? 1 : 0;
-        if (k0 + kk < md.ntm) {
+        if (real(k0 + kk)) {
           pmin = fmin(pmin, akk);
           pmax = fmax(pmax, akk);
         }
         ld += log(akk);
-        const double zr = P[(raug - k0) * PS + kk];
+        const double zr = P[(zrow - k0) * PS + kk];
         quad += zr * zr * r;
         ainv[kk] = r;
       }
       __syncthreads();
     }
+    if (pw < TM_PW) {   // columns past k_hi: no update from them
+      if (tid < TM_PW && tid >= pw) ainv[tid] = 0.0;
+      __syncthreads();
+    }
     // write the raw panel back (columns k0..k0+16, rows >= column)
     for (int e = tid; e < R * TM_PW; e += LBLK) {
       const int i = e / TM_PW, kk = e % TM_PW;
-      if (i >= kk) Gc[(size_t)(k0 + i) * mp + k0 + kk] = P[i * PS + kk];
+      if (i >= kk) Gout[(size_t)(k0 + i) * mp + k0 + kk] = P[i * PS + kk];
     }
     // trailing update of rows/cols >= k1 by MFMA tiles (wave-strided over lower tiles)
     const int k1 = k0 + TM_PW;
-    const int TR = (mp - k1) / 16;
-    const int ntile = TR * (TR + 1) / 2;
-    // TM_TILES tiles per wave per round, their loads issued first (the rounds were bound by
-    // one global load round trip per tile); tiles past ntile in the last round are masked
-    constexpr int NW = LBLK / 64;
-    for (int e0 = wv; e0 < ntile; e0 += TM_TILES * NW) {
-      int r0[TM_TILES], c0[TM_TILES];
-      bool in[TM_TILES];
-      v4d acc[TM_TILES];
+    if (k1 < k_hi || trail_all) {
+      const int TR = (mp - k1) / 16;
+      const int ntile = TR * (TR + 1) / 2;
+      // TM_TILES tiles per wave per round, their loads issued first (the rounds were bound by
+      // one global load round trip per tile); tiles past ntile in the last round are masked
+      constexpr int NW = LBLK / 64;
+      for (int e0 = wv; e0 < ntile; e0 += TM_TILES * NW) {
+        int r0[TM_TILES], c0[TM_TILES];
+        bool in[TM_TILES];
+        v4d acc[TM_TILES];
 #pragma unroll
-      for (int h = 0; h < TM_TILES; ++h) {
-        const int e = e0 + h * NW;
-        in[h] = e < ntile;
-        const int ee = in[h] ? e : e0;
-        int X = 0;
-        while ((X + 1) * (X + 2) / 2 <= ee) ++X;
-        const int Y = ee - X * (X + 1) / 2;
-        r0[h] = k1 + 16 * X;
-        c0[h] = k1 + 16 * Y;
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          acc[h][g] = Gin[(size_t)(r0[h] + (lane >> 4) + 4 * g) * mp + c0[h] + (lane & 15)];
-      }
-#pragma unroll
-      for (int h = 0; h < TM_TILES; ++h) {
-#pragma unroll
-        for (int k4 = 0; k4 < TM_PW / 4; ++k4) {
-          const int kk = 4 * k4 + (lane >> 4);
-          const double av = -P[(r0[h] - k0 + (lane & 15)) * PS + kk];
-          const double bv = P[(c0[h] - k0 + (lane & 15)) * PS + kk] * ainv[kk];
-          acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[h], 0, 0, 0);
-        }
-        if (in[h]) {
+        for (int h = 0; h < TM_TILES; ++h) {
+          const int e = e0 + h * NW;
+          in[h] = e < ntile;
+          const int ee = in[h] ? e : e0;
+          int X = 0;
+          while ((X + 1) * (X + 2) / 2 <= ee) ++X;
+          const int Y = ee - X * (X + 1) / 2;
+          r0[h] = k1 + 16 * X;
+          c0[h] = k1 + 16 * Y;
 #pragma unroll
           for (int g = 0; g < 4; ++g)
-            Gc[(size_t)(r0[h] + (lane >> 4) + 4 * g) * mp + c0[h] + (lane & 15)] = acc[h][g];
+            acc[h][g] = Gsrc[(size_t)(r0[h] + (lane >> 4) + 4 * g) * mp + c0[h] + (lane & 15)];
+        }
+#pragma unroll
+        for (int h = 0; h < TM_TILES; ++h) {
+#pragma unroll
+          for (int k4 = 0; k4 < TM_PW / 4; ++k4) {
+            const int kk = 4 * k4 + (lane >> 4);
+            const double av = -P[(r0[h] - k0 + (lane & 15)) * PS + kk];
+            const double bv = P[(c0[h] - k0 + (lane & 15)) * PS + kk] * ainv[kk];
+            acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[h], 0, 0, 0);
+          }
+          if (in[h]) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+              Gout[(size_t)(r0[h] + (lane >> 4) + 4 * g) * mp + c0[h] + (lane & 15)] = acc[h][g];
+          }
         }
       }
     }
     __syncthreads();
   }
-  if (tid == 0) {
+}
+
+__global__ void __launch_bounds__(LBLK) lg_tmelim(const DevModel* __restrict__ mds, LArgs a) {
+  const int c = blockIdx.x;
+  const DevModel& md = mds[ds_of(a, c)];
+  double* sc = a.s.sc + (size_t)c * 16;
+  // floor pass: only the chains whose b draw runs at the SVD noise floor, with Sigma + f I
+  const double fsh = a.floor_pass ? sc[SC_FLOOR] : 0.0;
+  if (a.floor_pass && !(fsh > 0.0)) return;
+  extern __shared__ double lsm[];
+  double* P = lsm;                     // [mp][TM_PW + 1]
+  __shared__ double ainv[TM_PW];
+  const int mp = md.mp, K0 = md.ntm_pad;
+  // G stays the Gram (the floor pass re-eliminates it); the factor and S0 go to G2
+  const double* Gg = a.s.G + (size_t)c * mp * mp;
+  double* Gc = a.s.G2 + (size_t)c * mp * mp;
+  double ld = 0.0, quad = 0.0, pmin = INFINITY, pmax = 0.0;
+  int fail = 0;
+  // timing-model prior 1/tm_weight on its diagonal, unit pivots on the pad columns
+  const int ntm = md.ntm;
+  const double tmp = md.tm_phiinv;
+  panel_ldl(Gg, Gc, mp, 0, K0, md.raug, true,
+            [&](int gk, double v) { return (gk < ntm) ? (v + tmp) + fsh : 1.0; },
+            [&](int gk) { return gk < ntm; }, P, ainv, ld, quad, pmin, pmax, fail);
+  if (threadIdx.x == 0) {
     sc[SC_LDTM] = ld;
     sc[SC_QUADTM] = quad;
     sc[SC_FAILTM] = (double)fail;
     sc[SC_TMPMIN] = pmin;
     sc[SC_TMPMAX] = pmax;
   }
-  (void)red;
 }
 
 // ------------------------------------------------------------------------------------
@@ -813,23 +845,31 @@ struct HyperLds {
   int SS;
 };
 
+// BIG (hyper class 1: blocks past HYPER_LDS_MAX columns, e.g. hundreds of ECORR epochs): the
+// same MH, likelihood and b draw with the block factored by panel_ldl into the chain's G3
+// instead of in LDS (S is then G3's hyper block, row stride mp).
+template <bool BIG>
 __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ mds, LArgs a) {
   const int c = blockIdx.x;
   const DevModel& md = mds[ds_of(a, c)];
-  if (hyper_class(md.nf + md.nec, a.hyper_lds) != 0) return;   // a lg_hyper_reg chain
+  if (hyper_class(md.nf + md.nec, a.hyper_lds) != (BIG ? 1 : 0)) return;   // another class's chain
   extern __shared__ double lsm[];
   // the hyper-dependent columns: Fourier (power law) then ECORR epochs (10^(2 ecorr_b))
   const int nf = md.nf + md.nec, K0 = md.ntm_pad, mp = md.mp;
   const int nfr = md.nf;
   const int ms = nf + 1;               // Fourier + ECORR block + augmented row
-  const int SS = ms + 1;
-  double* S = lsm;                     // [ms][SS]
-  double* ph = S + ms * SS;            // [nf] phi^-1
+  const int SS = BIG ? mp : ms + 1;
+  // LDS: S [ms][SS] (BIG: the panel [mp][TM_PW + 1] and 1 / a_kk [TM_PW] instead)
+  double* P = lsm;
+  double* S = BIG ? a.s.G3 + (size_t)blockIdx.x * mp * mp + (size_t)K0 * mp + K0 : lsm;
+  double* ainv = lsm + mp * (TM_PW + 1);
+  double* ph = BIG ? ainv + TM_PW : S + ms * SS;   // [nf] phi^-1
   double* vv = ph + nf;                // [ms] back-substitution accumulators / Delta
   double* wv_ = vv + ms;               // [ms] rhs
   __shared__ double red[4];
   __shared__ double mhv[NHYPER][4];
   __shared__ double bc[4];
+  __shared__ double hst[3];            // BIG: the factorisation's sum log a_kk, quad, failure
   const int tid = threadIdx.x;
   double* sc = a.s.sc + (size_t)c * 16;
   // floor pass: only the chains whose b draw runs at the SVD noise floor (SC_FLOOR > 0)
@@ -869,6 +909,26 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
       if (md.ec_count[b] > 0.0)
         logdet_phi += md.ec_count[b] * (2.0 * xget(q, md.ecorr_b[b]) * 2.302585092994045684);
     __syncthreads();
+    double ld = 0.0, quad = 0.0;
+    int fl = 0;
+    if constexpr (BIG) {
+      // blocked elimination of the hyper block (+ its augmented row) of S0 + diag(phi^-1):
+      // G2 -> G3 (the block and the augmented row are contiguous there, raug = K0 + nf)
+      double pmn = INFINITY, pmx = 0.0;
+      panel_ldl(Gc, S - ((size_t)K0 * mp + K0), mp, K0, K0 + nf, md.raug, false,
+                [&](int gk, double v) { return v + ph[gk - K0]; }, [](int) { return true; }, P,
+                ainv, ld, quad, pmn, pmx, fl);
+      if (tid == 0) {
+        hst[0] = ld;
+        hst[1] = quad;
+        hst[2] = (double)fl;
+      }
+      __syncthreads();
+      ld = hst[0];
+      quad = hst[1];
+      fl = hst[2] != 0.0;
+      __syncthreads();
+    } else {
     for (int e = tid; e < ms * ms; e += LBLK) {
       const int i = e / ms, j = e % ms;
       if (j > i) continue;
@@ -878,8 +938,6 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
       S[i * SS + j] = v;
     }
     __syncthreads();
-    double ld = 0.0, quad = 0.0;
-    int fl = 0;
     for (int k = 0; k < nf; ++k) {
       const double akk = S[k * SS + k];
       const double r = 1.0 / akk;
@@ -894,6 +952,7 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
         for (int j = j0; j <= i; j += 8) S[i * SS + j] -= lik * S[j * SS + k];
       }
       __syncthreads();
+    }
     }
     failed = fl | fail_tm;
     if (failed) return -INFINITY;

@@ -13,7 +13,7 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 # fixture-name prefix -> tests/golden/{prefix}_dataset.npz (tools/gen_golden.py)
 DATASETS = ("sim", "twob", "simclean", "scaled", "c3", "c4t", "c20", "tm22", "mb", "mbn",
-            "mid", "wide", "ecb", "ecn", "ecq")
+            "mid", "wide", "ecb", "ecn", "ecq", "ebig")
 
 CHAIN_KEYS = ("chain", "bchain", "zchain", "poutchain", "thetachain", "alphachain", "dfchain")
 

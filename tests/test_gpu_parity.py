@@ -46,7 +46,7 @@ def _native(ref, C, path="auto"):
     return ns
 
 
-@pytest.mark.parametrize("name", [n for n in NAMES if n.startswith(("ecb", "ecn", "ecq", "mb"))])
+@pytest.mark.parametrize("name", [n for n in NAMES if n.startswith(("ecb", "ecn", "ecq", "ebig", "mb"))])
 def test_general_white_noise_path_choice(name):
     """Per-backend efac / equad and ECORR models (gibbs.py:64-77) run on the persistent
     kernel's general white-noise instances when their hyper block fits (ecb / ecn: 20 Fourier +

@@ -455,6 +455,24 @@ def ecorr_classes(niter=12):
               np.nanmax(out["tape_b_cond"]), file=sys.stderr)
 
 
+def ecorr_big(niter=12):
+    """``ebig``: per-backend efac / equad / ECORR on 130 epochs x 2 sub-band TOAs (n = 260):
+    20 Fourier + 130 ECORR columns (m = 164), a red-noise / ECORR block past the large path's
+    LDS-resident one (gst_large.hpp HYPER_LDS_MAX = 138), which lg_hyper<true> factors in
+    global memory -- NANOGrav-style pulsars carry hundreds of ECORR epochs."""
+    psr = gdata.multiband(nepochs=130, nsub=2, seed=2446)
+    pta_e = PTA(psr, components=10, efac=(0.2, 10.0), selection="backend",
+                log10_ecorr=(-8.5, -5.0))
+    x0 = [1.1, -6.5, -6.6, 0.9, -6.8, -7.0, 4.33, -14.0]
+    np.savez_compressed(os.path.join(OUTDIR, "ebig_dataset.npz"), **dataset_arrays(pta_e, psr))
+    for j, name in enumerate(("beta", "t")):
+        out = run_one(pta_e, name, MODELS[name], seed=8300 + 13 * j, niter=niter, x0=x0)
+        out["model_kw"] = np.array(repr(MODELS[name]))
+        np.savez_compressed(os.path.join(OUTDIR, f"ref_ebig_{name}_fixed.npz"), **out)
+        print("ebig", name, "P", len(x0), "m", pta_e.m, "n_ecorr", pta_e.n_ecorr, "cond:",
+              np.nanmax(out["tape_b_cond"]), file=sys.stderr)
+
+
 def mid(niter=12):
     """A mid-size pulsar for the register-resident kernel's wide TOA instances (NS = 6, 8
     slots of 64 TOAs): 130 J1713+0747 epochs x 3 sub-band TOAs (gdata.multiband, one
@@ -499,6 +517,9 @@ def main():
         return
     if "--only-ecorr-classes" in sys.argv:
         ecorr_classes(12)
+        return
+    if "--only-ecorr-big" in sys.argv:
+        ecorr_big(12)
         return
     if "--only-mid" in sys.argv:
         mid(12)
@@ -563,6 +584,7 @@ def main():
     general(niter)
     small_ecorr(niter)
     ecorr_classes(niter)
+    ecorr_big(niter)
     mid(niter)
     wide(niter)
 

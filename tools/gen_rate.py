@@ -2,6 +2,7 @@
 persistent kernel's GEN instances against the large path, same dataset and start.
 
     python tools/gen_rate.py [sweeps] [datasets]     e.g. python tools/gen_rate.py 200 ecb,ecq
+    (GR_PATHS=large: the large path only, e.g. for ebig's 150-column red-noise / ECORR block)
 
 Datasets are the golden ones (tests/golden/<name>_dataset.npz); the model is bench.py's
 (outlier mixture, beta theta prior, varied nu), chains start from prior draws.
@@ -44,7 +45,7 @@ def main():
     for nm in names:
         pta = load_dataset(dataset=nm)
         for C in (512, 2048):
-            for path in ("persistent", "large"):
+            for path in os.environ.get("GR_PATHS", "persistent,large").split(","):
                 r, ok = rate(pta, path, C, S)
                 row = dict(dataset=nm, n=pta.n, m=pta.m, P=len(pta.params), chains=C, path=path,
                            sweeps=S, chain_sweeps_per_s=r, status_ok=ok)
