@@ -22,7 +22,12 @@ def main():
     n = int(sys.argv[3]) if len(sys.argv) > 3 else 100_000
     comp = int(sys.argv[4]) if len(sys.argv) > 4 else 60
     ntm = int(sys.argv[5]) if len(sys.argv) > 5 else 300
-    pta = PTA(data.scaled_synthetic(n=n, components=comp, ntm=ntm, seed=5), components=comp)
+    if os.environ.get("RL_DATASET"):   # a golden dataset instead, e.g. RL_DATASET=ebig
+        sys.path.insert(0, "tests")
+        from golden_io import load_dataset
+        pta = load_dataset(dataset=os.environ["RL_DATASET"])
+    else:
+        pta = PTA(data.scaled_synthetic(n=n, components=comp, ntm=ntm, seed=5), components=comp)
     ns = NativeSampler(pta, CFG, 0)
     ns.alloc(C)
     ns.set_state(**initial_state(pta, C, 0))
