@@ -63,7 +63,10 @@ __host__ __device__ constexpr int hyper_class(int hcols, int force_lds) {
                                : (force_lds ? 0 : (hcols <= 8 * 8 - 2 ? 8 : (hcols <= 8 * 16 - 2 ? 16 : 0)));
 }
 constexpr int GRAM_WAVES = 8;  // chains per gram workgroup
-constexpr int TM_PW = 16;      // panel width of the timing-model elimination
+#ifndef GST_TM_PW
+#define GST_TM_PW 16   // A/B builds override it (32: config-5 tmelim 1.75 -> 2.95 ms, ebig -20%)
+#endif
+constexpr int TM_PW = GST_TM_PW;   // panel width of the blocked eliminations (panel_ldl)
 constexpr int TM_TILES = 4;   // trailing-update tiles per wave per round (lg_tmelim)
 
 struct LScratch {
