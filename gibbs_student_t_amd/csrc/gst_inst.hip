@@ -17,8 +17,7 @@ kfn_t kfn() {
   return &gst_sweep_kernel<MT, NS, K0, RA, TAPE, WPB, OCC, PAIR, GEN>;
 }
 
-// GEN shapes (the general white-noise model) have one-chain-per-SIMD instances only: no
-// two-chains-per-SIMD build (occ2 is ignored) and no pair mode (the host never asks for it)
+// GEN shapes (the general white-noise model): no pair mode (the host never asks for it)
 template <int MT, int NS, int K0, int RA, int GEN>
 kfn_t pick_shape(bool tape, int wpb, bool occ2, bool pair) {
   if constexpr (GEN != 0) {
@@ -26,6 +25,7 @@ kfn_t pick_shape(bool tape, int wpb, bool occ2, bool pair) {
     if (tape) return kfn<MT, NS, K0, RA, true, 4, 1, false, true>();
     if (wpb == 1) return kfn<MT, NS, K0, RA, false, 1, 1, false, true>();
     if (wpb == 2) return kfn<MT, NS, K0, RA, false, 2, 1, false, true>();
+    if (occ2 && occ_for(MT, K0) == 2) return kfn<MT, NS, K0, RA, false, 4, 2, false, true>();
     return kfn<MT, NS, K0, RA, false, 4, 1, false, true>();
   } else {
     if (tape) return kfn<MT, NS, K0, RA, true>();

@@ -216,7 +216,7 @@ int gst_sync(void* ctx, void* stream);
  * columns, 26 with <= 24, n <= 1024 for the 30-component / 16-column shape; smaller models
  * run padded with unit-prior dummy columns; the general white-noise model -- per-backend
  * efac / equad, ECORR columns, up to 8 parameters -- with <= 16 timing-model columns, up to
- * 60 Fourier + ECORR columns and n <= 512, one chain per SIMD); the
+ * 60 Fourier + ECORR columns and n <= 512); the
  * large path runs
  * each sweep as a pipeline of kernels (fp64-MFMA Gram shared by all chains, blocked
  * timing-model elimination, LDS-resident red-noise MH, MFMA T b, per-TOA passes) for
