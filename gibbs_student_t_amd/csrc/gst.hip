@@ -521,10 +521,12 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
   // TOA slots of 64 held in registers: 2, 3, 4 (J1713-sized), 6, 8 (mid-size, n <= 512),
   // 12, 16 (wide mid-size, n <= 1024: the run_sims model's shape only; these keep one chain
   // per SIMD, their two-chains-per-SIMD builds would spill kilobytes per lane)
-  // (the general white-noise model: 2, 4, 8)
-  const int NS = gen ? (nsl <= 2 ? 2 : (nsl <= 4 ? 4 : 8)) :
-                 (nsl <= 2 ? 2 : (nsl <= 3 ? 3 : (nsl <= 4 ? 4 : (nsl <= 6 ? 6 : (nsl <= 8 ? 8 :
-                 (nsl <= 12 ? 12 : 16))))));
+  // (the general white-noise model: 2, 3 (MT = 10 only), 4, 8); the smallest instantiated
+  // slot count that holds n
+  static const int kSlots[] = {2, 3, 4, 6, 8, 12, 16};
+  int NS = 16;
+  for (int ns : kSlots)
+    if (ns >= nsl && sh && pick(MT, ns, K0, raug, gen, false, 4, false)) { NS = ns; break; }
   const bool fits = sh && (classic(d) || gen) && round_up(nmax, 4) <= 64 * NS &&
                     pick(MT, NS, K0, raug, gen, false, 4, false);
   int path = cx->path_req;

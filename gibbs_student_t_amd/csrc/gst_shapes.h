@@ -39,6 +39,7 @@ typedef void (*kfn_t)(const DevModel*, const DevState, const DevRec, const DevTa
   X(8, 2, 2, 62, 1) /* general white noise: <= 46 Fourier + ECORR columns, n <= 128 */ \
   X(8, 4, 2, 62, 1)                                                                \
   X(10, 2, 2, 76, 1) /* <= 60 Fourier + ECORR columns */                           \
+  X(10, 3, 2, 76, 1) /* J1713+0747 with per-backend efac / equad: n = 130 */          \
   X(10, 4, 2, 76, 1)                                                               \
   X(10, 8, 2, 76, 1)
 

@@ -13,7 +13,7 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 # fixture-name prefix -> tests/golden/{prefix}_dataset.npz (tools/gen_golden.py)
 DATASETS = ("sim", "twob", "simclean", "scaled", "c3", "c4t", "c20", "tm22", "mb", "mbn",
-            "mid", "wide", "ecb", "ecn", "ecq", "ebig")
+            "mid", "wide", "ecb", "ecn", "ecq", "ebig", "jb")
 
 CHAIN_KEYS = ("chain", "bchain", "zchain", "poutchain", "thetachain", "alphachain", "dfchain")
 
@@ -32,7 +32,7 @@ def load_dataset(efac=False, dataset="j1713"):
                                efac=(0.2, 10.0) if int(d["efac_varied"]) else 1.0,
                                backends=d["backends"], selection=str(d["selection"]),
                                n_ecorr=int(d["n_ecorr"]), ecorr_backend=d["ecorr_backend"],
-                               log10_ecorr=tuple(d["log10_ecorr"]))
+                               log10_ecorr=tuple(d["log10_ecorr"]) or None)
     return PTA.from_arrays("J1713+0747", d["residuals"], d["toaerrs"], d["T"], d["Ffreqs"],
                            int(d["components"]), float(d["tm_weight"]),
                            efac=(0.2, 10.0) if efac else 1.0)

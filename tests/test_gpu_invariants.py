@@ -23,14 +23,14 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-# (+ the general white-noise instances: two backends with ECORR, one backend with ECORR;
-# these have no two-waves-per-chain build)
+# (+ the general white-noise instances: two backends with ECORR, one backend with ECORR,
+# J1713+0747 with two backends and no ECORR; these have no two-waves-per-chain build)
 FIXTURES = ("beta_efac_fixed", "c3_beta_fixed", "tm22_beta_fixed", "vvh17_prior",
-            "ecb_beta_fixed", "ecq_t_fixed")
+            "ecb_beta_fixed", "ecq_t_fixed", "jb_uniform_fixed")
 
 
 def _skip_pair(name, build):
-    if build == "pair" and name.startswith("ec"):
+    if build == "pair" and name.startswith(("ec", "jb")):
         pytest.skip("general white-noise model: one wave per chain only")
 
 
@@ -111,7 +111,7 @@ def test_poisoned_lds_and_scratch_change_nothing(name, build):
 
 
 @pytest.mark.parametrize("name", ["beta_fixed", "t_prior", "uniform_fixed", "beta_efac_fixed",
-                                  "ecq_beta_fixed", "ecq_t_fixed"])
+                                  "ecq_beta_fixed", "ecq_t_fixed", "jb_beta_fixed"])
 def test_low_rank_gram_matches_mfma_gram(name):
     """The persistent kernel's low-rank Gram (one noise class on J1713: the class Gram plus a
     rank-1 update per flagged TOA) against its MFMA Gram

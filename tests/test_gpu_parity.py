@@ -46,14 +46,17 @@ def _native(ref, C, path="auto"):
     return ns
 
 
-@pytest.mark.parametrize("name", [n for n in NAMES if n.startswith(("ecb", "ecn", "ecq", "ebig", "mb"))])
+@pytest.mark.parametrize("name", [n for n in NAMES
+                                  if n.startswith(("ecb", "ecn", "ecq", "ebig", "mb", "jb"))])
 def test_general_white_noise_path_choice(name):
     """Per-backend efac / equad and ECORR models (gibbs.py:64-77) run on the persistent
     kernel's general white-noise instances when their hyper block fits (ecb / ecn: 20 Fourier +
-    24 ECORR columns), on the large path otherwise (mb / mbn: 80 columns)."""
+    24 ECORR columns; jb: J1713+0747 with per-backend efac / equad, 60 Fourier columns and
+    n = 130 on the three-slot instance), on the large path otherwise (mb / mbn: 80 columns;
+    ebig: 150)."""
     ref = load_ref(name)
     ns = NativeSampler(ref["pta"], ref["kw"], 0)
-    assert ns.path == ("persistent" if name.startswith("ec") else "large")
+    assert ns.path == ("persistent" if name.startswith(("ecb", "ecn", "ecq", "jb")) else "large")
     if ns.path == "persistent":
         # no two-waves-per-chain build for these models: asking for it fails loudly
         ns.alloc(8)

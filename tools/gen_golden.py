@@ -288,7 +288,7 @@ def dataset_arrays(pta, psr):
         out.update(backends=np.asarray(psr.backends).astype(str), selection=pta.selection,
                    n_ecorr=pta.n_ecorr, ecorr_backend=pta.ecorr_backend,
                    efac_varied=int(pta.efac_const is None),
-                   log10_ecorr=np.array([-8.5, -5.0]))
+                   log10_ecorr=np.array([-8.5, -5.0] if pta.n_ecorr else []))
     return out
 
 
@@ -473,6 +473,28 @@ def ecorr_big(niter=12):
               np.nanmax(out["tape_b_cond"]), file=sys.stderr)
 
 
+def j1713_backends(niter=12):
+    """``jb``: the headline pulsar (J1713+0747's 130 epochs, run_sims' 30 red-noise
+    components and 14-column timing model, m = 74) with per-backend efac / equad and no
+    ECORR: the first half of the epochs on ASP, the rest on GUPPI (P = 6).  J1713's error
+    bars are all one value, so the model has two noise classes (backend x error bar) and
+    the persistent kernel's general white-noise instances take their class paths."""
+    psr = gdata.j1713(seed=1714, theta=0.05)
+    order = np.argsort(psr.toas)
+    labels = np.empty(psr.n, dtype="<U5")
+    labels[order] = np.where(np.arange(psr.n) < psr.n // 2, "ASP", "GUPPI")
+    psr.backends = labels
+    pta = PTA(psr, efac=(0.2, 10.0), selection="backend")
+    x0 = [1.1, -6.5, 0.9, -7.0, 4.33, -14.0]   # ASP efac, equad, GUPPI efac, equad, gamma, A
+    np.savez_compressed(os.path.join(OUTDIR, "jb_dataset.npz"), **dataset_arrays(pta, psr))
+    for j, name in enumerate(("beta", "uniform")):
+        out = run_one(pta, name, MODELS[name], seed=8500 + 13 * j, niter=niter, x0=x0)
+        out["model_kw"] = np.array(repr(MODELS[name]))
+        np.savez_compressed(os.path.join(OUTDIR, f"ref_jb_{name}_fixed.npz"), **out)
+        print("jb", name, "P", len(x0), "m", pta.m, "cond:",
+              np.nanmax(out["tape_b_cond"]), file=sys.stderr)
+
+
 def mid(niter=12):
     """A mid-size pulsar for the register-resident kernel's wide TOA instances (NS = 6, 8
     slots of 64 TOAs): 130 J1713+0747 epochs x 3 sub-band TOAs (gdata.multiband, one
@@ -520,6 +542,9 @@ def main():
         return
     if "--only-ecorr-big" in sys.argv:
         ecorr_big(12)
+        return
+    if "--only-j1713-backends" in sys.argv:
+        j1713_backends(12)
         return
     if "--only-mid" in sys.argv:
         mid(12)
@@ -585,6 +610,7 @@ def main():
     small_ecorr(niter)
     ecorr_classes(niter)
     ecorr_big(niter)
+    j1713_backends(niter)
     mid(niter)
     wide(niter)
 
