@@ -40,7 +40,7 @@ def rate(pta, path, C, S, W=20):
 
 def main():
     S = int(sys.argv[1]) if len(sys.argv) > 1 else 200
-    names = (sys.argv[2] if len(sys.argv) > 2 else "ecb,ecq").split(",")
+    names = (sys.argv[2] if len(sys.argv) > 2 else "ecb,ecq,jb").split(",")
     out = []
     for nm in names:
         pta = load_dataset(dataset=nm)
