@@ -56,8 +56,9 @@ struct Ctx {
   // large path: scratch sized for scratch_C chains, per-kernel timing events
   gst::LScratch ls{};
   int scratch_C = 0;
-  size_t lds_tm = 0, lds_hyper = 0, lds_btm = 0, lds_hyper_big = 0;
+  size_t lds_tm = 0, lds_hyper = 0, lds_btm = 0, lds_hyper_big = 0, lds_hyper_ec = 0;
   bool hyper_big = false;          // large path: a hyper block past HYPER_LDS_MAX (G3 scratch)
+  bool hyper_ec = false;           // ... of ECORR epochs, eliminated first (lg_hyper<2>, no G3)
   bool timing = false;
   std::vector<hipEvent_t> evpool;
   std::vector<int> evkind;  // kind of event pair i (events 2i, 2i+1)
@@ -540,13 +541,20 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
     return fail(b);
   }
   if (path == GST_PATH_LARGE) {
-    // hyper blocks past HYPER_LDS_MAX columns are factored in global memory (lg_hyper<true>),
-    // whose LDS holds a 16-column panel of all mp rows plus three vectors of the block
+    // hyper blocks past HYPER_LDS_MAX columns: ECORR epochs around a small timing-model +
+    // Fourier block are eliminated first (lg_hyper<2>), other blocks are factored in global
+    // memory (lg_hyper<1>), whose LDS holds a 16-column panel of all mp rows plus three vectors
     const int ms = nf + nec + 1, mpl = round_up(round_up(ntm > 0 ? ntm : 1, 16) + nf + nec + 1, 16);
-    if (nf + nec > gst::HYPER_LDS_MAX &&
+    const int hc = gst::hyper_class(nf + nec, 0, nec, ntm + nf + 1), qx = ntm + nf + 1;
+    if (hc == 1 &&
         (size_t)(mpl * (gst::TM_PW + 1) + gst::TM_PW + nf + nec + 2 * ms) * 8 > 160 * 1024)
       return fail("gst_model_set: large path: basis too large for the LDS panel of the "
                   "red-noise / ECORR block elimination");
+    // lg_hyper<2> (ECORR epochs eliminated first): its LDS vectors span the basis
+    if (hc == 2 && (size_t)(qx * (qx + 1) + nf + 2 * nec + 4 * mpl + gst::EC_ECH * (qx + 1)) * 8 >
+                       160 * 1024)
+      return fail("gst_model_set: large path: too many ECORR epochs for the LDS of their "
+                  "elimination");
   }
   free_model(cx);
   // large path: timing-model block padded to whole 16-column MFMA tiles, no dummies
@@ -573,26 +581,40 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
   cx->WPB = 4;
   cx->gen = path == GST_PATH_PERSISTENT && gen;
   cx->path = path;
+  cx->hyper_big = cx->hyper_ec = false;
   if (path == GST_PATH_LARGE) {
     const gst::DevModel& h = hmd[0];
     cx->raug = h.raug;
     cx->lds_tm = (size_t)h.mp * (gst::TM_PW + 1) * 8;
     const int ms = h.nf + h.nec + 1;
-    cx->hyper_big = h.nf + h.nec > gst::HYPER_LDS_MAX;
-    cx->lds_hyper = cx->hyper_big ? 0 : (size_t)(ms * (ms + 1) + h.nf + h.nec + 2 * ms) * 8;
+    const int hc = gst::hyper_class_of(h, 0);
+    // lg_hyper<1> runs for class 1, and for class 2 under GST_DEBUG_LARGE_HYPER (its G3
+    // scratch is then allocated at the first such launch)
+    cx->hyper_big = gst::hyper_class_of(h, 1) == 1;
+    cx->hyper_ec = hc == 2;
+    cx->lds_hyper = hc == 1 || hc == 2 ? 0 : (size_t)(ms * (ms + 1) + h.nf + h.nec + 2 * ms) * 8;
     cx->lds_hyper_big = (size_t)(h.mp * (gst::TM_PW + 1) + gst::TM_PW + h.nf + h.nec + 2 * ms) * 8;
+    // lg_hyper<2>: X [qx][qx + 1], phi^-1 [nf + nec], four vectors of mp, a_e [nec], one
+    // chunk of couplings [EC_ECH][qx] and its 1 / a_e
+    const int qx = h.ntm + h.nf + 1;
+    cx->lds_hyper_ec = (size_t)(qx * (qx + 1) + h.nf + h.nec + 4 * h.mp + h.nec +
+                                gst::EC_ECH * qx + gst::EC_ECH) * 8;
     cx->lds_btm = (size_t)(3 * h.ntm_pad + h.raug) * 8;
     HIP_OK(hipFuncSetAttribute((const void*)gst::lg_gram,
                                hipFuncAttributeMaxDynamicSharedMemorySize, gst::GRAM_LDS * 8));
     HIP_OK(hipFuncSetAttribute((const void*)gst::lg_tmelim,
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)cx->lds_tm));
-    if (!cx->hyper_big)
-      HIP_OK(hipFuncSetAttribute((const void*)gst::lg_hyper<false>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)cx->lds_hyper));
-    else
-      HIP_OK(hipFuncSetAttribute((const void*)gst::lg_hyper<true>,
+    if (cx->hyper_big && cx->lds_hyper_big <= 160 * 1024)
+      HIP_OK(hipFuncSetAttribute((const void*)gst::lg_hyper<1>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)cx->lds_hyper_big));
+    if (hc == 2)
+      HIP_OK(hipFuncSetAttribute((const void*)gst::lg_hyper<2>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)cx->lds_hyper_ec));
+    if (!cx->hyper_big)
+      HIP_OK(hipFuncSetAttribute((const void*)gst::lg_hyper<0>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)cx->lds_hyper));
     HIP_OK(hipFuncSetAttribute((const void*)gst::lg_btm,
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)cx->lds_btm));
   }
@@ -648,7 +670,15 @@ static int large_ys(const Ctx* cx) {
 }
 
 static int ensure_scratch(Ctx* cx, int C, hipStream_t st) {
-  if (C <= cx->scratch_C) return 0;
+  // lg_hyper<1>'s G3: class-1 models, and class-2 ones under GST_DEBUG_LARGE_HYPER
+  const bool need_g3 = cx->hyper_big && (!cx->hyper_ec || (cx->debug & GST_DEBUG_LARGE_HYPER));
+  if (C <= cx->scratch_C && (!need_g3 || cx->ls.G3)) return 0;
+  if (C <= cx->scratch_C) {
+    const size_t mp = cx->hmd[0].mp;
+    HIP_OK(hipMallocAsync((void**)&cx->ls.G3, (size_t)cx->scratch_C * mp * mp * 8, st));
+    HIP_OK(hipMemsetAsync(cx->ls.G3, 0, (size_t)cx->scratch_C * mp * mp * 8, st));
+    return 0;
+  }
   free_scratch(cx, st);
   const gst::DevModel& h = cx->hmd[0];
   const size_t mp = h.mp, npad = large_ys(cx);
@@ -662,7 +692,7 @@ static int ensure_scratch(Ctx* cx, int C, hipStream_t st) {
   HIP_OK(hipMemsetAsync(cx->ls.G2, 0, (size_t)C * mp * mp * 8, st));
   HIP_OK(hipMemsetAsync(cx->ls.sc, 0, (size_t)C * 16 * 8, st));
   HIP_OK(hipMemsetAsync(cx->ls.v, 0, (size_t)C * mp * 8, st));
-  if (cx->hyper_big) {   // lg_hyper<true>'s factor of the red-noise / ECORR block
+  if (need_g3) {   // lg_hyper<1>'s factor of the red-noise / ECORR block
     HIP_OK(hipMallocAsync((void**)&cx->ls.G3, (size_t)C * mp * mp * 8, st));
     HIP_OK(hipMemsetAsync(cx->ls.G3, 0, (size_t)C * mp * mp * 8, st));
   }
@@ -672,7 +702,7 @@ static int ensure_scratch(Ctx* cx, int C, hipStream_t st) {
 
 // The red-noise MH block's launches: one per hyper kernel class present (gst_large.hpp
 // hyper_class); a chain of another class returns at once.
-static int launch_hyper(Ctx* cx, gst::LArgs& a, const bool (&hcls)[4], dim3 g8, dim3 b8,
+static int launch_hyper(Ctx* cx, gst::LArgs& a, const bool (&hcls)[5], dim3 g8, dim3 b8,
                         dim3 g16, dim3 b16, dim3 g_chain, dim3 b_chain, hipStream_t st) {
   if (hcls[0]) {
     a.kclass = 8;
@@ -684,11 +714,15 @@ static int launch_hyper(Ctx* cx, gst::LArgs& a, const bool (&hcls)[4], dim3 g8, 
   }
   if (hcls[2]) {
     a.kclass = 0;
-    LG_LAUNCH(GST_K_HYPER, gst::lg_hyper<false>, g_chain, b_chain, cx->lds_hyper);
+    LG_LAUNCH(GST_K_HYPER, gst::lg_hyper<0>, g_chain, b_chain, cx->lds_hyper);
   }
   if (hcls[3]) {
     a.kclass = 1;
-    LG_LAUNCH(GST_K_HYPER, gst::lg_hyper<true>, g_chain, b_chain, cx->lds_hyper_big);
+    LG_LAUNCH(GST_K_HYPER, gst::lg_hyper<1>, g_chain, b_chain, cx->lds_hyper_big);
+  }
+  if (hcls[4]) {
+    a.kclass = 2;
+    LG_LAUNCH(GST_K_HYPER, gst::lg_hyper<2>, g_chain, b_chain, cx->lds_hyper_ec);
   }
   return 0;
 }
@@ -713,12 +747,12 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
   // elimination (lg_hyper_reg<8> / <16>); larger ones: lg_hyper (LDS)
   const int hyper_lds = (cx->debug & GST_DEBUG_LARGE_HYPER) ? 1 : 0;
   bool wcls[3] = {false, false, false}, tcls[2] = {false, false};
-  bool hcls[4] = {false, false, false, false};
+  bool hcls[5] = {false, false, false, false, false};
   for (const gst::DevModel& hm : cx->hmd) {
     wcls[gst::white_class(hm.npad)] = true;
     tcls[gst::toa_class(hm.npad)] = true;
-    const int hc = gst::hyper_class(hm.nf + hm.nec, hyper_lds);
-    hcls[hc == 8 ? 0 : (hc == 16 ? 1 : (hc == 0 ? 2 : 3))] = true;
+    const int hc = gst::hyper_class_of(hm, hyper_lds);
+    hcls[hc == 8 ? 0 : (hc == 16 ? 1 : (hc == 0 ? 2 : (hc == 1 ? 3 : 4)))] = true;
   }
   a.hyper_lds = hyper_lds;
   const dim3 g_hr8((C + gst::HR<8>::WPB - 1) / gst::HR<8>::WPB), b_hr8(64 * gst::HR<8>::WPB);

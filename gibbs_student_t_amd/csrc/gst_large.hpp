@@ -49,8 +49,10 @@ constexpr int TBLK_WAVE_NPAD = 8192;
 //   lg_white: 0 = one wave (npad <= TBLK_WAVE_NPAD), 1 = TBLK_SMALL, 2 = TBLK threads;
 //   lg_toa:   0 = TBLK_SMALL, 1 = TBLK threads;
 //   hyper:    8 / 16 = lg_hyper_reg<8 / 16> (hyper block of <= 62 / 126 columns), 0 = lg_hyper
-//             (LDS-resident block, <= HYPER_LDS_MAX columns), 1 = lg_hyper<true> (larger blocks,
-//             e.g. hundreds of ECORR epochs: blocked elimination in global memory).
+//             (LDS-resident block, <= HYPER_LDS_MAX columns), 1 = lg_hyper<1> (larger blocks:
+//             blocked elimination in global memory), 2 = lg_hyper<2> (larger blocks made of
+//             ECORR epochs -- hundreds of them -- around a small timing-model + Fourier block:
+//             the epochs eliminated first, see lg_hyper).
 __host__ __device__ constexpr int white_class(int npad) {
   return npad <= TBLK_WAVE_NPAD ? 0 : (npad <= TBLK_SMALL_NPAD ? 1 : 2);
 }
@@ -58,9 +60,20 @@ __host__ __device__ constexpr int toa_class(int npad) { return npad <= TBLK_SMAL
 // hyper class from the dataset's own hyper block nf + nec: lg_hyper_reg<MT> takes up to
 // HR<MT>::RA = 8 MT - 2 columns (62 / 126)
 constexpr int HYPER_LDS_MAX = 138;   // lg_hyper's LDS block: (ms (ms + 1) + 3 ms) doubles < 160 KB
-__host__ __device__ constexpr int hyper_class(int hcols, int force_lds) {
-  return hcols > HYPER_LDS_MAX ? 1
+// lg_hyper<2>: the timing-model + Fourier + augmented-row block it factors per likelihood
+// (qx = ntm + nfourier + 1 rows) is at most EC_QX_MAX (its pairs sit in EC_NPR registers of
+// each of LBLK threads); the epochs' couplings stream through LDS EC_ECH epochs at a time
+constexpr int EC_QX_MAX = 76;
+constexpr int EC_NPR = 12;
+constexpr int EC_ECH = 32;
+static_assert(EC_QX_MAX * (EC_QX_MAX + 1) / 2 <= EC_NPR * LBLK, "lg_hyper<2> pair registers");
+// (force_lds: GST_DEBUG_LARGE_HYPER, the generic kernels: class 0, or 1 past HYPER_LDS_MAX)
+__host__ __device__ constexpr int hyper_class(int hcols, int force_lds, int nec, int qx) {
+  return hcols > HYPER_LDS_MAX ? ((nec > 0 && qx <= EC_QX_MAX && !force_lds) ? 2 : 1)
                                : (force_lds ? 0 : (hcols <= 8 * 8 - 2 ? 8 : (hcols <= 8 * 16 - 2 ? 16 : 0)));
+}
+__host__ __device__ inline int hyper_class_of(const DevModel& md, int force_lds) {
+  return hyper_class(md.nf + md.nec, force_lds, md.nec, md.ntm + md.nf + 1);
 }
 constexpr int GRAM_WAVES = 8;  // chains per gram workgroup
 #ifndef GST_TM_PW
@@ -76,7 +89,7 @@ struct LScratch {
   double* w;   // [C][npad]  1/N (white scratch: y^2/a during the white block)
   double* sc;  // [C][16]    per-chain scalars (SC_*)
   double* v;   // [C][mp]    b-draw solution (internal order)
-  double* G3;  // [C][mp*mp] lg_hyper<true>'s factor of the hyper block (null unless needed)
+  double* G3;  // [C][mp*mp] lg_hyper<1>'s factor of the hyper block (null unless needed)
 };
 enum : int {
   SC_LOGDETN = 0,
@@ -816,6 +829,7 @@ __global__ void __launch_bounds__(LBLK) lg_tmelim(const DevModel* __restrict__ m
   // floor pass: only the chains whose b draw runs at the SVD noise floor, with Sigma + f I
   const double fsh = a.floor_pass ? sc[SC_FLOOR] : 0.0;
   if (a.floor_pass && !(fsh > 0.0)) return;
+  if (hyper_class_of(md, a.hyper_lds) == 2) return;   // lg_hyper<2> factors the timing model
   extern __shared__ double lsm[];
   double* P = lsm;                     // [mp][TM_PW + 1]
   __shared__ double ainv[TM_PW];
@@ -848,27 +862,65 @@ struct HyperLds {
   int SS;
 };
 
-// BIG (hyper class 1: blocks past HYPER_LDS_MAX columns, e.g. hundreds of ECORR epochs): the
-// same MH, likelihood and b draw with the block factored by panel_ldl into the chain's G3
-// instead of in LDS (S is then G3's hyper block, row stride mp).
-template <bool BIG>
+// MODE 1 (BIG, hyper class 1: blocks past HYPER_LDS_MAX columns): the same MH, likelihood
+// and b draw with the block factored by panel_ldl into the chain's G3 instead of in LDS (S is
+// then G3's hyper block, row stride mp).
+//
+// MODE 2 (EC, hyper class 2: such blocks made of ECORR epochs around a timing-model + Fourier
+// block of at most EC_QX_MAX rows -- NANOGrav-style pulsars, one ECORR column per observing
+// epoch): Sigma is eliminated epochs first, in the order [ECORR | TM | Fourier], from the raw
+// Gram G.  Epochs share no TOA, so the ECORR block of T^T N^-1 T is diagonal and eliminating it
+// costs no fill: pivots a_e = G_ee + phi_e^-1, and the rest becomes
+//   X = G_xx + diag(phi_x^-1) - sum_e G_xe G_ex / a_e      (x: TM, Fourier, augmented row)
+// factored densely in LDS.  Per likelihood that is O(nec qx^2) + O(qx^3) work instead of the
+// (nf + nec)^3 of MODE 1; lg_tmelim does nothing for these chains (the timing model is part
+// of X, so its prior enters per likelihood) and this kernel draws all of b (lg_btm skips
+// them).  Same variates (Philox by internal column), MH decisions and outputs otherwise.
+template <int MODE>
 __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ mds, LArgs a) {
+  constexpr bool BIG = MODE == 1, EC = MODE == 2;
   const int c = blockIdx.x;
   const DevModel& md = mds[ds_of(a, c)];
-  if (hyper_class(md.nf + md.nec, a.hyper_lds) != (BIG ? 1 : 0)) return;   // another class's chain
+  if (hyper_class_of(md, a.hyper_lds) != MODE) return;   // another class's chain
   extern __shared__ double lsm[];
   // the hyper-dependent columns: Fourier (power law) then ECORR epochs (10^(2 ecorr_b))
   const int nf = md.nf + md.nec, K0 = md.ntm_pad, mp = md.mp;
-  const int nfr = md.nf;
+  const int nfr = md.nf, nec = md.nec, ntm = md.ntm;
   const int ms = nf + 1;               // Fourier + ECORR block + augmented row
-  const int SS = BIG ? mp : ms + 1;
-  // LDS: S [ms][SS] (BIG: the panel [mp][TM_PW + 1] and 1 / a_kk [TM_PW] instead)
+  // EC: X's rows: ntm timing-model columns, nfr Fourier columns, the augmented row (nxd = qx-1)
+  const int qx = ntm + nfr + 1, nxd = qx - 1;
+  const int SS = BIG ? mp : (EC ? qx + 1 : ms + 1);
+  // LDS: S [ms][SS] (BIG: the panel [mp][TM_PW + 1] and 1 / a_kk [TM_PW] instead; EC: X
+  // [qx][SS], then the vectors below sized mp, the pivots a_e, one chunk of couplings)
   double* P = lsm;
   double* S = BIG ? a.s.G3 + (size_t)blockIdx.x * mp * mp + (size_t)K0 * mp + K0 : lsm;
   double* ainv = lsm + mp * (TM_PW + 1);
-  double* ph = BIG ? ainv + TM_PW : S + ms * SS;   // [nf] phi^-1
-  double* vv = ph + nf;                // [ms] back-substitution accumulators / Delta
-  double* wv_ = vv + ms;               // [ms] rhs
+  double* ph = BIG ? ainv + TM_PW : S + (EC ? qx : ms) * SS;   // [nf] phi^-1
+  const int vlen = EC ? mp : ms;
+  double* vv = ph + nf;                // [vlen] back-substitution accumulators / Delta
+  double* wv_ = vv + vlen;             // [vlen] rhs
+  double* aE = wv_ + vlen;             // EC: [nec] epoch pivots a_e
+  double* Ech = aE + nec;              // EC: [EC_ECH][qx] couplings G_ex of one chunk of epochs
+  double* einv = Ech + EC_ECH * qx;    // EC: [EC_ECH] 1 / a_e of the chunk
+  double* dl = einv + EC_ECH;          // EC: [mp] Delta (tape mode), internal order
+  double* vfull = dl + mp;             // EC: [mp] the b draw, internal order
+  const double* Gg = a.s.G + (size_t)c * mp * mp;   // EC: the raw Gram (lower triangle)
+  // EC: internal column of X's row i, and G at (r, q) from the lower triangle
+  auto gx = [&](int i) { return i < ntm ? i : (i < nxd ? K0 + (i - ntm) : md.raug); };
+  auto Gl = [&](int r, int q) { return r >= q ? Gg[(size_t)r * mp + q] : Gg[(size_t)q * mp + r]; };
+  // EC: this thread's (row, column) pairs of X's lower triangle
+  int pi_[EC ? EC_NPR : 1], pj_[EC ? EC_NPR : 1];
+  if constexpr (EC) {
+#pragma unroll
+    for (int s2 = 0; s2 < EC_NPR; ++s2) {
+      const int p = threadIdx.x + LBLK * s2;
+      int i = (int)((sqrt(8.0 * p + 1.0) - 1.0) * 0.5);
+      while (i * (i + 1) / 2 > p) --i;
+      while ((i + 1) * (i + 2) / 2 <= p) ++i;
+      pi_[s2] = p < qx * (qx + 1) / 2 ? i : -1;
+      pj_[s2] = p - i * (i + 1) / 2;
+    }
+  }
   __shared__ double red[4];
   __shared__ double mhv[NHYPER][4];
   __shared__ double bc[4];
@@ -884,8 +936,9 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
   XVec xv;
   load_x(md, a.st, c, xv);
   const double logdetN = sc[SC_LOGDETN], rNr = sc[SC_RNR];
-  const double ld_tm = sc[SC_LDTM], quad_tm = sc[SC_QUADTM];
-  const int fail_tm = sc[SC_FAILTM] != 0.0;
+  // (EC: the timing model is factored with the rest, lg_tmelim left these untouched)
+  const double ld_tm = EC ? 0.0 : sc[SC_LDTM], quad_tm = EC ? 0.0 : sc[SC_QUADTM];
+  const int fail_tm = EC ? 0 : sc[SC_FAILTM] != 0.0;
   const double x_last0 = sc[SC_XLAST];
   int status = fail_tm ? 1 : 0;
   if (!a.eval_only && !a.floor_pass && tid < NHYPER) mh_variate(md, rng, tp, NWHITE + tid, mhv[tid]);
@@ -914,7 +967,75 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
     __syncthreads();
     double ld = 0.0, quad = 0.0;
     int fl = 0;
-    if constexpr (BIG) {
+    if constexpr (EC) {
+      // X -= sum_e G_xe G_ex / a_e over chunks of EC_ECH epochs (each thread: its pairs)
+      double acc[EC_NPR];
+#pragma unroll
+      for (int s2 = 0; s2 < EC_NPR; ++s2) acc[s2] = 0.0;
+      for (int e0 = 0; e0 < nec; e0 += EC_ECH) {
+        const int ne = nec - e0 < EC_ECH ? nec - e0 : EC_ECH;
+        for (int t = tid; t < ne * qx; t += LBLK) {
+          const int ee = t / qx, i = t - ee * qx;
+          Ech[ee * qx + i] = Gl(K0 + nfr + e0 + ee, gx(i));
+        }
+        if (tid < ne) {
+          const int ge = K0 + nfr + e0 + tid;
+          const double ae = Gg[(size_t)ge * mp + ge] + ph[nfr + e0 + tid];
+          aE[e0 + tid] = ae;
+          einv[tid] = 1.0 / ae;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s2 = 0; s2 < EC_NPR; ++s2) {
+          if (pi_[s2] < 0) continue;
+          const double* ci = Ech + pi_[s2];
+          const double* cj = Ech + pj_[s2];
+          double t2 = acc[s2];
+          for (int ee = 0; ee < ne; ++ee) t2 += ci[ee * qx] * (cj[ee * qx] * einv[ee]);
+          acc[s2] = t2;
+        }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < EC_NPR; ++s2) {
+        const int i = pi_[s2], j = pj_[s2];
+        if (i < 0) continue;
+        double v = Gg[(size_t)gx(i) * mp + gx(j)];
+        if (i == j && i < nxd) v = (i < ntm) ? (v + md.tm_phiinv) + fsh : v + ph[i - ntm];
+        S[i * SS + j] = v - acc[s2];
+      }
+      // the epochs' pivots and augmented-row terms
+      double lde = 0.0, qde = 0.0, fle = 0.0;
+      for (int e = tid; e < nec; e += LBLK) {
+        const double ae = aE[e];
+        const double zr = Gg[(size_t)md.raug * mp + K0 + nfr + e];
+        fle += !(ae > 0.0) ? 1.0 : 0.0;
+        lde += log(ae);
+        qde += zr * zr * (1.0 / ae);
+      }
+      lde = block_sum(lde, red);
+      qde = block_sum(qde, red);
+      fle = block_sum(fle, red);
+      __syncthreads();
+      // dense LDL^T of X (rows i in (k, nxd], cols j in (k, i]: 32 row groups x 8 col groups)
+      for (int k = 0; k < nxd; ++k) {
+        const double akk = S[k * SS + k];
+        const double r = 1.0 / akk;
+        const double zr = S[nxd * SS + k];
+        fl |= !(akk > 0.0) ? 1 : 0;
+        ld += log(akk);
+        quad += zr * zr * r;
+        const int i0 = k + 1 + (tid >> 3), j0 = k + 1 + (tid & 7);
+        for (int i = i0; i < qx; i += 32) {
+          const double lik = S[i * SS + k] * r;
+          for (int j = j0; j <= i; j += 8) S[i * SS + j] -= lik * S[j * SS + k];
+        }
+        __syncthreads();
+      }
+      ld += lde;
+      quad += qde;
+      fl |= fle != 0.0 ? 1 : 0;
+    } else if constexpr (BIG) {
       // blocked elimination of the hyper block (+ its augmented row) of S0 + diag(phi^-1):
       // G2 -> G3 (the block and the augmented row are contiguous there, raug = K0 + nf)
       double pmn = INFINITY, pmx = 0.0;
@@ -1030,9 +1151,20 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
   double fs = 0.0;
   if (!a.floor_pass && redraw && !fb && !(a.st.debug & DEBUG_EXACT_BDRAW)) {
     double mn = INFINITY, mx = 0.0;
-    for (int k = tid; k < nf; k += LBLK) {
-      mn = fmin(mn, S[k * SS + k]);
-      mx = fmax(mx, S[k * SS + k]);
+    if constexpr (EC) {   // the epochs' pivots, then X's (timing model and Fourier)
+      for (int e = tid; e < nec; e += LBLK) {
+        mn = fmin(mn, aE[e]);
+        mx = fmax(mx, aE[e]);
+      }
+      for (int k = tid; k < nxd; k += LBLK) {
+        mn = fmin(mn, S[k * SS + k]);
+        mx = fmax(mx, S[k * SS + k]);
+      }
+    } else {
+      for (int k = tid; k < nf; k += LBLK) {
+        mn = fmin(mn, S[k * SS + k]);
+        mx = fmax(mx, S[k * SS + k]);
+      }
     }
     mx = wave_max(mx);
     mn = -wave_max(-mn);
@@ -1041,8 +1173,12 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
       bc[tid >> 6] = mn;
     }
     __syncthreads();
-    mx = fmax(fmax(fmax(red[0], red[1]), fmax(red[2], red[3])), sc[SC_TMPMAX]);
-    mn = fmin(fmin(fmin(bc[0], bc[1]), fmin(bc[2], bc[3])), sc[SC_TMPMIN]);
+    mx = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+    mn = fmin(fmin(bc[0], bc[1]), fmin(bc[2], bc[3]));
+    if constexpr (!EC) {   // (the timing model's, from lg_tmelim)
+      mx = fmax(mx, sc[SC_TMPMAX]);
+      mn = fmin(mn, sc[SC_TMPMIN]);
+    }
     fs = floor_of(mn, mx);
     __syncthreads();
   }
@@ -1057,6 +1193,60 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
                        ((fs > 0.0 && !a.floor_pass) ? STATUS_FLOOR_COUNT : 0);
   }
   if (!redraw || fb || fs > 0.0) return;   // fs > 0: the floor pass draws b
+  if constexpr (EC) {
+    // b draw, all of it: X's columns by back substitution through X's factor, then each
+    // epoch e from its pivot and its couplings to X: v_e = (w_e - y_e sum_x G_xe v_x) y_e,
+    // w = zraw y + eta as below (Philox normals by internal column)
+    if (tp) {
+      for (int i = tid; i < mp; i += LBLK) dl[i] = 0.0;
+      __syncthreads();
+      for (int j = tid; j < md.m; j += LBLK) dl[md.ref2int[j]] = tp[TP_DELTA + j];
+      __syncthreads();
+    }
+    for (int k = tid; k < nxd; k += LBLK) {
+      const double yk = rsqrt_nr(S[k * SS + k]);
+      if (tp) {
+        double s = 0.0;
+        for (int i = k; i < nxd; ++i) s += S[i * SS + k] * dl[gx(i)];
+        wv_[k] = (S[nxd * SS + k] + s) * yk;
+      } else {
+        wv_[k] = S[nxd * SS + k] * yk + normal_k(rng, (uint32_t)gx(k), TAG_BDRAW);
+      }
+      vv[k] = 0.0;
+    }
+    __syncthreads();
+    for (int i = nxd - 1; i >= 0; --i) {
+      if (tid == 0) {
+        const double yi = rsqrt_nr(S[i * SS + i]);
+        bc[0] = (wv_[i] - yi * vv[i]) * yi;
+      }
+      __syncthreads();
+      const double vi = bc[0];
+      if (tid == 0) vfull[gx(i)] = vi;
+      for (int k = tid; k < i; k += LBLK) vv[k] += S[i * SS + k] * vi;
+      __syncthreads();
+    }
+    for (int e = tid; e < nec; e += LBLK) {
+      const int ge = K0 + nfr + e;
+      const double ae = aE[e], ye = rsqrt_nr(ae);
+      double sx = 0.0;
+      for (int i = 0; i < nxd; ++i) sx += Gl(gx(i), ge) * vfull[gx(i)];
+      const double zr = Gg[(size_t)md.raug * mp + ge];
+      double we;
+      if (tp) {
+        double s = ae * dl[ge];
+        for (int i = 0; i < nxd; ++i) s += Gl(gx(i), ge) * dl[gx(i)];
+        we = (zr + s) * ye;
+      } else {
+        we = zr * ye + normal_k(rng, (uint32_t)ge, TAG_BDRAW);
+      }
+      vfull[ge] = (we - ye * sx) * ye;
+    }
+    __syncthreads();
+    for (int j = tid; j < md.m; j += LBLK)
+      a.st.b[(size_t)c * md.m + j] = vfull[md.ref2int[j]];
+    return;
+  }
   // b draw, Fourier block: w_k = zraw_k y_k + eta_k, then L^T v = w (raw columns, pivots on
   // the diagonal, y_k = 1/sqrt(a_kk)); back substitution in axpy form over rows of S
   double* vF = a.s.v + (size_t)c * mp + K0;
@@ -1135,7 +1325,7 @@ __global__ void __launch_bounds__(64 * HR<MT>::WPB) lg_hyper_reg(const DevModel*
   const int c = blockIdx.x * WPB + wv;
   if (c >= a.C) return;
   const DevModel& md = mds[ds_of(a, c)];
-  if (hyper_class(md.nf + md.nec, a.hyper_lds) != MT) return;  // another class's chain
+  if (hyper_class_of(md, a.hyper_lds) != MT) return;  // another class's chain
   double* S0R = smem[wv];
   double* colq = S0R + H::S0;
   double* junk = colq + 8 * MT;
@@ -1382,6 +1572,7 @@ __global__ void __launch_bounds__(LBLK) lg_btm(const DevModel* __restrict__ mds,
   const int tid = threadIdx.x;
   const double* sc = a.s.sc + (size_t)c * 16;
   if (sc[SC_REDRAW] == 0.0 || sc[SC_FB] != 0.0) return;
+  if (hyper_class_of(md, a.hyper_lds) == 2) return;   // lg_hyper<2> drew all of b
   const double* Gc = a.s.G2 + (size_t)c * mp * mp;   // lg_tmelim's factor (K0 > 0 here)
   double* v = a.s.v + (size_t)c * mp;
   const Rng rng = make_rng(a, c);

@@ -245,7 +245,9 @@ int gst_set_waves(void* ctx, int waves);
  * one-wave-per-chain Gram (lg_gram_small) would run; the two give bitwise the same G.
  * GST_DEBUG_LARGE_HYPER forces the LDS-resident hyper kernel (lg_hyper) where the register-
  * resident one (lg_hyper_reg) would run: same variates and decisions, likelihoods within
- * rounding.  Test switches (the defaults are the faster kernels). */
+ * rounding; and the blocked global-memory elimination (lg_hyper<1>) where the ECORR-epochs-
+ * first one (lg_hyper<2>) would run: likelihoods within rounding, b draws of the same law.
+ * Test switches (the defaults are the faster kernels). */
 /* GST_DEBUG_EXACT_BDRAW: every b draw is the exact draw from Sigma, also beyond fp64
  * resolution (no SVD noise floor, see gst_sweep). */
 /* GST_DEBUG_MFMA_GRAM (ABI 5): the persistent kernel computes every Gram on the MFMA path,

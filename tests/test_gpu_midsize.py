@@ -124,3 +124,78 @@ def test_register_hyper_matches_lds_hyper_ecorr(name):
     for k in ("alpha", "pout", "theta"):
         d = np.abs(a[k] - b[k])
         assert np.all(d <= 1e-8 * np.maximum(np.abs(b[k]), 1e-300) + 1e-300), (k, d.max())
+
+
+@pytest.mark.parametrize("name", ["ebig_beta_fixed", "ebig_t_fixed"])
+def test_epochs_first_hyper_matches_blocked_hyper(name):
+    """ebig (20 Fourier + 130 ECORR epochs, 14 timing-model columns): the epochs-first
+    elimination lg_hyper<2> (hyper class 2, the default) against the blocked global-memory one
+    lg_hyper<1> (GST_DEBUG_LARGE_HYPER) -- the b-marginalised likelihood at 256 states (prior
+    draws of x, the fixture's latents) within 1e-10 relative.  The two factor Sigma in
+    different orders, so their Philox b draws are different (equally distributed) draws and
+    the chains are compared with the reference instead: test_gpu_parity.py's large-path
+    likelihood, MH / b-draw (recorded draw term) and replay tests run on lg_hyper<2>."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    from golden_io import load_ref, sweep_state
+    ref = load_ref(name)
+    pta = ref["pta"]
+    s0 = sweep_state(ref, 0)
+    C2 = 256
+    lo = np.array([p.pmin for p in pta.params])
+    hi = np.array([p.pmax for p in pta.params])
+    x = np.random.default_rng(5).uniform(lo, hi, size=(C2, len(lo)))
+    got = []
+    for large_hyper in (False, True):
+        ns = NativeSampler(pta, ref["kw"], 0, path="large")
+        ns.set_debug(large_hyper=large_hyper)
+        ns.alloc(C2)
+        ns.set_state(x=x, b=np.tile(s0["b"], (C2, 1)), z=np.tile(s0["z"], (C2, 1)),
+                     alpha=np.tile(s0["alpha"], (C2, 1)), pout=np.tile(s0["pout"], (C2, 1)),
+                     theta=np.full(C2, s0["theta"]), nu=np.full(C2, s0["nu"]))
+        w, h = ns.eval_lnlike()
+        got.append((np.asarray(w), np.asarray(h)))
+        ns.close()
+    (w2, h2), (w1, h1) = got
+    np.testing.assert_array_equal(w2, w1)
+    ok = np.isfinite(h1)
+    assert ok.sum() > C2 // 2
+    np.testing.assert_array_equal(np.isfinite(h2), ok)
+    r = np.abs(h2[ok] - h1[ok]) / np.abs(h1[ok])
+    assert r.max() <= 1e-10, r.max()
+
+
+def test_epochs_first_hyper_draws_match_blocked_hyper():
+    """The two eliminations' Philox b draws are different draws of one law, so chains of the
+    same start through lg_hyper<2> and lg_hyper<1> must have the same marginal law at every
+    sweep (converged or not): 1024 ebig chains from prior draws, after 150 sweeps, every
+    sampled parameter plus theta, nu and two b components, two-sample KS p > 1e-3."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    import scipy.stats
+    from golden_io import load_dataset
+    from gibbs_student_t_amd.run_sims import MODELS
+    pta = load_dataset(dataset="ebig")
+    C2, S2 = 1024, 150
+    lo = np.array([p.pmin for p in pta.params])
+    hi = np.array([p.pmax for p in pta.params])
+    x0 = np.random.default_rng(9).uniform(lo, hi, size=(C2, len(lo)))
+    fin = []
+    for large_hyper in (False, True):
+        ns = NativeSampler(pta, MODELS["beta"], 0, path="large")
+        ns.set_debug(large_hyper=large_hyper)
+        ns.alloc(C2)
+        ns.set_state(x=x0, z=np.zeros((C2, pta.n)), alpha=np.ones((C2, pta.n)),
+                     theta=np.full(C2, 0.05), nu=np.full(C2, 4.0))
+        ns.sweep(S2, seed=91)
+        st = ns.get_state()
+        ns.close()
+        assert np.all((st["status"] & STATUS_ERRORS) == 0)
+        fin.append(st)
+    a, b = fin
+    series = [(f"x{j}", a["x"][:, j], b["x"][:, j]) for j in range(len(lo))]
+    series += [("theta", a["theta"], b["theta"]), ("nu", a["nu"], b["nu"]),
+               ("b_fourier0", a["b"][:, 0], b["b"][:, 0]), ("b_last", a["b"][:, -1], b["b"][:, -1])]
+    for nm, u, v in series:
+        p = scipy.stats.ks_2samp(u, v).pvalue
+        assert p > 1e-3, f"{nm}: KS p = {p:.2e} (means {u.mean():.4g} / {v.mean():.4g})"
