@@ -61,12 +61,14 @@ __host__ __device__ constexpr int toa_class(int npad) { return npad <= TBLK_SMAL
 // HR<MT>::RA = 8 MT - 2 columns (62 / 126)
 constexpr int HYPER_LDS_MAX = 138;   // lg_hyper's LDS block: (ms (ms + 1) + 3 ms) doubles < 160 KB
 // lg_hyper<2>: the timing-model + Fourier + augmented-row block it factors per likelihood
-// (qx = ntm + nfourier + 1 rows) is at most EC_QX_MAX (its pairs sit in EC_NPR registers of
-// each of LBLK threads); the epochs' couplings stream through LDS EC_ECH epochs at a time
+// (qx = ntm + nfourier + 1 rows) is at most EC_QX_MAX (its lower 16x16 tiles, at most
+// EC_TPW per wave, accumulate in MFMA registers); the epochs' couplings stream through LDS
+// EC_ECH epochs at a time
 constexpr int EC_QX_MAX = 76;
-constexpr int EC_NPR = 12;
+constexpr int EC_TPW = 4;
 constexpr int EC_ECH = 32;
-static_assert(EC_QX_MAX * (EC_QX_MAX + 1) / 2 <= EC_NPR * LBLK, "lg_hyper<2> pair registers");
+static_assert(((EC_QX_MAX + 15) / 16) * ((EC_QX_MAX + 15) / 16 + 1) / 2 <= EC_TPW * (LBLK / 64),
+              "lg_hyper<2> tiles per wave");
 // (force_lds: GST_DEBUG_LARGE_HYPER, the generic kernels: class 0, or 1 past HYPER_LDS_MAX)
 __host__ __device__ constexpr int hyper_class(int hcols, int force_lds, int nec, int qx) {
   return hcols > HYPER_LDS_MAX ? ((nec > 0 && qx <= EC_QX_MAX && !force_lds) ? 2 : 1)
@@ -888,39 +890,48 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
   const int nfr = md.nf, nec = md.nec, ntm = md.ntm;
   const int ms = nf + 1;               // Fourier + ECORR block + augmented row
   // EC: X's rows: ntm timing-model columns, nfr Fourier columns, the augmented row (nxd = qx-1)
-  const int qx = ntm + nfr + 1, nxd = qx - 1;
+  const int qx = ntm + nfr + 1, nxd = qx - 1, qxp = (qx + 15) & ~15;
   const int SS = BIG ? mp : (EC ? qx + 1 : ms + 1);
   // LDS: S [ms][SS] (BIG: the panel [mp][TM_PW + 1] and 1 / a_kk [TM_PW] instead; EC: X
-  // [qx][SS], then the vectors below sized mp, the pivots a_e, one chunk of couplings)
+  // [qx][SS] and its epochs-eliminated base XB [qx][SS], then the vectors below sized mp, the
+  // pivots a_e, one chunk of couplings [EC_ECH][qxp])
   double* P = lsm;
   double* S = BIG ? a.s.G3 + (size_t)blockIdx.x * mp * mp + (size_t)K0 * mp + K0 : lsm;
   double* ainv = lsm + mp * (TM_PW + 1);
-  double* ph = BIG ? ainv + TM_PW : S + (EC ? qx : ms) * SS;   // [nf] phi^-1
+  double* XB = S + qx * SS;            // EC: G_xx - sum_e G_xe G_ex / a_e (no priors)
+  double* ph = BIG ? ainv + TM_PW : S + (EC ? 2 * qx : ms) * SS;   // [nf] phi^-1
   const int vlen = EC ? mp : ms;
   double* vv = ph + nf;                // [vlen] back-substitution accumulators / Delta
   double* wv_ = vv + vlen;             // [vlen] rhs
   double* aE = wv_ + vlen;             // EC: [nec] epoch pivots a_e
-  double* Ech = aE + nec;              // EC: [EC_ECH][qx] couplings G_ex of one chunk of epochs
-  double* einv = Ech + EC_ECH * qx;    // EC: [EC_ECH] 1 / a_e of the chunk
+  double* Ech = aE + nec;              // EC: [EC_ECH][qxp] couplings G_ex of a chunk of epochs
+  double* einv = Ech + EC_ECH * qxp;   // EC: [EC_ECH] 1 / a_e of the chunk
   double* dl = einv + EC_ECH;          // EC: [mp] Delta (tape mode), internal order
   double* vfull = dl + mp;             // EC: [mp] the b draw, internal order
   const double* Gg = a.s.G + (size_t)c * mp * mp;   // EC: the raw Gram (lower triangle)
   // EC: internal column of X's row i, and G at (r, q) from the lower triangle
   auto gx = [&](int i) { return i < ntm ? i : (i < nxd ? K0 + (i - ntm) : md.raug); };
   auto Gl = [&](int r, int q) { return r >= q ? Gg[(size_t)r * mp + q] : Gg[(size_t)q * mp + r]; };
-  // EC: this thread's (row, column) pairs of X's lower triangle
-  int pi_[EC ? EC_NPR : 1], pj_[EC ? EC_NPR : 1];
+  // EC: this wave's lower 16x16 tiles of X (tile t = wave + 4 h, rows r0_, columns c0_)
+  int r0_[EC ? EC_TPW : 1], c0_[EC ? EC_TPW : 1];
+  bool tin_[EC ? EC_TPW : 1];
   if constexpr (EC) {
+    const int TR = qxp / 16, ntile = TR * (TR + 1) / 2;
 #pragma unroll
-    for (int s2 = 0; s2 < EC_NPR; ++s2) {
-      const int p = threadIdx.x + LBLK * s2;
-      int i = (int)((sqrt(8.0 * p + 1.0) - 1.0) * 0.5);
-      while (i * (i + 1) / 2 > p) --i;
-      while ((i + 1) * (i + 2) / 2 <= p) ++i;
-      pi_[s2] = p < qx * (qx + 1) / 2 ? i : -1;
-      pj_[s2] = p - i * (i + 1) / 2;
+    for (int h = 0; h < EC_TPW; ++h) {
+      const int t = (threadIdx.x >> 6) + (LBLK / 64) * h;
+      tin_[h] = t < ntile;
+      int X = 0;
+      while ((X + 1) * (X + 2) / 2 <= t) ++X;
+      r0_[h] = 16 * X;
+      c0_[h] = 16 * (t - X * (X + 1) / 2);
     }
   }
+  // EC: the ECORR parameters XB, a_e and the epochs' likelihood terms (ecs) were made for
+  __shared__ double eck[NBMAX];
+  __shared__ double ecs[3];
+  __shared__ int ecvalid;
+  if (EC && threadIdx.x == 0) ecvalid = 0;
   __shared__ double red[4];
   __shared__ double mhv[NHYPER][4];
   __shared__ double bc[4];
@@ -968,73 +979,138 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
     double ld = 0.0, quad = 0.0;
     int fl = 0;
     if constexpr (EC) {
-      // X -= sum_e G_xe G_ex / a_e over chunks of EC_ECH epochs (each thread: its pairs)
-      double acc[EC_NPR];
+      // XB = G_xx - sum_e G_xe G_ex / a_e: recomputed only when an ECORR parameter changed
+      // since the last factorisation (a proposal of log10_A or gamma reuses it)
+      bool same = ecvalid != 0;
+      for (int b = 0; b < md.nb; ++b) same = same && xget(q, md.ecorr_b[b]) == eck[b];
+      if (!same) {
+        // chunks of EC_ECH epochs: A = (G_ex / a_e)^T, B = G_ex on the MFMA, k = epochs
+        const int lane = tid & 63;
+        v4d acc[EC_TPW];
 #pragma unroll
-      for (int s2 = 0; s2 < EC_NPR; ++s2) acc[s2] = 0.0;
-      for (int e0 = 0; e0 < nec; e0 += EC_ECH) {
-        const int ne = nec - e0 < EC_ECH ? nec - e0 : EC_ECH;
-        for (int t = tid; t < ne * qx; t += LBLK) {
-          const int ee = t / qx, i = t - ee * qx;
-          Ech[ee * qx + i] = Gl(K0 + nfr + e0 + ee, gx(i));
-        }
-        if (tid < ne) {
-          const int ge = K0 + nfr + e0 + tid;
-          const double ae = Gg[(size_t)ge * mp + ge] + ph[nfr + e0 + tid];
-          aE[e0 + tid] = ae;
-          einv[tid] = 1.0 / ae;
-        }
-        __syncthreads();
+        for (int h = 0; h < EC_TPW; ++h) acc[h] = v4d{0.0, 0.0, 0.0, 0.0};
+        for (int e0 = 0; e0 < nec; e0 += EC_ECH) {
+          const int ne = nec - e0 < EC_ECH ? nec - e0 : EC_ECH;
+          for (int t = tid; t < EC_ECH * qxp; t += LBLK) {
+            const int ee = t / qxp, i = t - ee * qxp;
+            Ech[t] = (ee < ne && i < qx) ? Gl(K0 + nfr + e0 + ee, gx(i)) : 0.0;
+          }
+          if (tid < EC_ECH) {
+            double r = 0.0;
+            if (tid < ne) {
+              const int ge = K0 + nfr + e0 + tid;
+              const double ae = Gg[(size_t)ge * mp + ge] + ph[nfr + e0 + tid];
+              aE[e0 + tid] = ae;
+              r = 1.0 / ae;
+            }
+            einv[tid] = r;
+          }
+          __syncthreads();
 #pragma unroll
-        for (int s2 = 0; s2 < EC_NPR; ++s2) {
-          if (pi_[s2] < 0) continue;
-          const double* ci = Ech + pi_[s2];
-          const double* cj = Ech + pj_[s2];
-          double t2 = acc[s2];
-          for (int ee = 0; ee < ne; ++ee) t2 += ci[ee * qx] * (cj[ee * qx] * einv[ee]);
-          acc[s2] = t2;
+          for (int h = 0; h < EC_TPW; ++h) {
+            if (!tin_[h]) continue;
+#pragma unroll
+            for (int k4 = 0; k4 < EC_ECH / 4; ++k4) {
+              const int kk = 4 * k4 + (lane >> 4);
+              const double av = Ech[kk * qxp + r0_[h] + (lane & 15)] * einv[kk];
+              const double bv = Ech[kk * qxp + c0_[h] + (lane & 15)];
+              acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[h], 0, 0, 0);
+            }
+          }
+          __syncthreads();
+        }
+#pragma unroll
+        for (int h = 0; h < EC_TPW; ++h) {
+          if (!tin_[h]) continue;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int i = r0_[h] + (lane >> 4) + 4 * g, j = c0_[h] + (lane & 15);
+            if (i < qx && j <= i) XB[i * SS + j] = Gg[(size_t)gx(i) * mp + gx(j)] - acc[h][g];
+          }
+        }
+        // the epochs' pivots and augmented-row terms
+        double lde = 0.0, qde = 0.0, fle = 0.0;
+        for (int e = tid; e < nec; e += LBLK) {
+          const double ae = aE[e];
+          const double zr = Gg[(size_t)md.raug * mp + K0 + nfr + e];
+          fle += !(ae > 0.0) ? 1.0 : 0.0;
+          lde += log(ae);
+          qde += zr * zr * (1.0 / ae);
+        }
+        lde = block_sum(lde, red);
+        qde = block_sum(qde, red);
+        fle = block_sum(fle, red);
+        if (tid == 0) {
+          ecs[0] = lde;
+          ecs[1] = qde;
+          ecs[2] = fle;
+          for (int b = 0; b < md.nb; ++b) eck[b] = xget(q, md.ecorr_b[b]);
+          ecvalid = 1;
         }
         __syncthreads();
       }
-#pragma unroll
-      for (int s2 = 0; s2 < EC_NPR; ++s2) {
-        const int i = pi_[s2], j = pj_[s2];
-        if (i < 0) continue;
-        double v = Gg[(size_t)gx(i) * mp + gx(j)];
+      // X = XB + the timing-model and Fourier priors
+      for (int t = tid; t < qx * qx; t += LBLK) {
+        const int i = t / qx, j = t - i * qx;
+        if (j > i) continue;
+        double v = XB[i * SS + j];
         if (i == j && i < nxd) v = (i < ntm) ? (v + md.tm_phiinv) + fsh : v + ph[i - ntm];
-        S[i * SS + j] = v - acc[s2];
+        S[i * SS + j] = v;
       }
-      // the epochs' pivots and augmented-row terms
-      double lde = 0.0, qde = 0.0, fle = 0.0;
-      for (int e = tid; e < nec; e += LBLK) {
-        const double ae = aE[e];
-        const double zr = Gg[(size_t)md.raug * mp + K0 + nfr + e];
-        fle += !(ae > 0.0) ? 1.0 : 0.0;
-        lde += log(ae);
-        qde += zr * zr * (1.0 / ae);
-      }
-      lde = block_sum(lde, red);
-      qde = block_sum(qde, red);
-      fle = block_sum(fle, red);
+      const double lde = ecs[0], qde = ecs[1], fle = ecs[2];
       __syncthreads();
-      // dense LDL^T of X (rows i in (k, nxd], cols j in (k, i]: 32 row groups x 8 col groups)
-      for (int k = 0; k < nxd; ++k) {
-        const double akk = S[k * SS + k];
-        const double r = 1.0 / akk;
-        const double zr = S[nxd * SS + k];
-        fl |= !(akk > 0.0) ? 1 : 0;
-        ld += log(akk);
-        quad += zr * zr * r;
-        const int i0 = k + 1 + (tid >> 3), j0 = k + 1 + (tid & 7);
-        for (int i = i0; i < qx; i += 32) {
-          const double lik = S[i * SS + k] * r;
-          for (int j = j0; j <= i; j += 8) S[i * SS + j] -= lik * S[j * SS + k];
+      // dense LDL^T of X, two columns per barrier: the trailing block (rows i, cols j <= i
+      // past k + 1: 32 row groups x 8 col groups) takes columns k and k + 1 at once, each
+      // thread forming column k + 1's updated entries c_i = S_i,k+1 - S_ik S_k+1,k / a_kk
+      // itself; column k + 1 itself is written back in the next round (no thread reads it
+      // there).  The pivots' logs and the augmented row's terms after the loop, one column
+      // per thread (a pivot and its row entry are final once their column is eliminated).
+      auto wback = [&](int kd) {   // column kd's update by column kd - 1
+        const double s10r = S[kd * SS + kd - 1] * (1.0 / S[(kd - 1) * SS + kd - 1]);
+        for (int i = kd + tid; i < qx; i += LBLK) S[i * SS + kd] -= S[i * SS + kd - 1] * s10r;
+      };
+      int kd = -1;
+      for (int k = 0; k < nxd; k += 2) {
+        if (kd >= 0) wback(kd);
+        if (k + 1 < nxd) {
+          const double r0 = 1.0 / S[k * SS + k];
+          const double s10r = S[(k + 1) * SS + k] * r0;
+          const double r1 = 1.0 / (S[(k + 1) * SS + k + 1] - S[(k + 1) * SS + k] * s10r);
+          const int i0 = k + 2 + (tid >> 3), j0 = k + 2 + (tid & 7);
+          for (int i = i0; i < qx; i += 32) {
+            const double sik = S[i * SS + k];
+            const double li0 = sik * r0, li1 = (S[i * SS + k + 1] - sik * s10r) * r1;
+            for (int j = j0; j <= i; j += 8) {
+              const double sjk = S[j * SS + k];
+              S[i * SS + j] -= li0 * sjk + li1 * (S[j * SS + k + 1] - sjk * s10r);
+            }
+          }
+          kd = k + 1;
+        } else {
+          const double r = 1.0 / S[k * SS + k];
+          const int i0 = k + 1 + (tid >> 3), j0 = k + 1 + (tid & 7);
+          for (int i = i0; i < qx; i += 32) {
+            const double lik = S[i * SS + k] * r;
+            for (int j = j0; j <= i; j += 8) S[i * SS + j] -= lik * S[j * SS + k];
+          }
+          kd = -1;
         }
         __syncthreads();
       }
-      ld += lde;
-      quad += qde;
-      fl |= fle != 0.0 ? 1 : 0;
+      if (kd >= 0) {
+        wback(kd);
+        __syncthreads();
+      }
+      double ldx = 0.0, qdx = 0.0, flx = 0.0;
+      for (int k = tid; k < nxd; k += LBLK) {
+        const double akk = S[k * SS + k], zr = S[nxd * SS + k];
+        flx += !(akk > 0.0) ? 1.0 : 0.0;
+        ldx += log(akk);
+        qdx += zr * zr * (1.0 / akk);
+      }
+      ld = block_sum(ldx, red) + lde;
+      quad = block_sum(qdx, red) + qde;
+      fl = (block_sum(flx, red) != 0.0 || fle != 0.0) ? 1 : 0;
     } else if constexpr (BIG) {
       // blocked elimination of the hyper block (+ its augmented row) of S0 + diag(phi^-1):
       // G2 -> G3 (the block and the augmented row are contiguous there, raug = K0 + nf)
