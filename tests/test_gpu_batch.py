@@ -26,7 +26,7 @@ from test_gpu_parity import assert_replay_matches  # noqa: E402
 # ragged no_outlier twin (n = 119 next to n = 130)
 REPLAY = [n for n in fixture_names()
           if "fixed" in n and "vvh17" not in n and "efac" not in n
-          and not n.startswith(("scaled", "c20", "tm22", "mb", "ec", "ebig"))]   # one basis shape per batch
+          and not n.startswith(("scaled", "c20", "tm22", "mb", "ec", "ebig", "jb"))]   # one basis shape per batch
 
 
 def _pad(a, nst):
