@@ -592,7 +592,8 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
     // scratch is then allocated at the first such launch)
     cx->hyper_big = gst::hyper_class_of(h, 1) == 1;
     cx->hyper_ec = hc == 2;
-    cx->lds_hyper = hc == 1 || hc == 2 ? 0 : (size_t)(ms * (ms + 1) + h.nf + h.nec + 2 * ms) * 8;
+    const bool lds_fits = h.nf + h.nec <= gst::HYPER_LDS_MAX;   // lg_hyper<0> (also forced)
+    cx->lds_hyper = lds_fits ? (size_t)(ms * (ms + 1) + h.nf + h.nec + 2 * ms) * 8 : 0;
     cx->lds_hyper_big = (size_t)(h.mp * (gst::TM_PW + 1) + gst::TM_PW + h.nf + h.nec + 2 * ms) * 8;
     // lg_hyper<2>: X and XB [qx][qx + 1], phi^-1 [nf + nec], four vectors of mp, a_e [nec],
     // one chunk of couplings [EC_ECH][qxp] and its 1 / a_e
@@ -612,7 +613,7 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
       HIP_OK(hipFuncSetAttribute((const void*)gst::lg_hyper<2>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)cx->lds_hyper_ec));
-    if (!cx->hyper_big)
+    if (lds_fits)
       HIP_OK(hipFuncSetAttribute((const void*)gst::lg_hyper<0>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)cx->lds_hyper));
     HIP_OK(hipFuncSetAttribute((const void*)gst::lg_btm,

@@ -60,7 +60,7 @@ __host__ __device__ constexpr int toa_class(int npad) { return npad <= TBLK_SMAL
 // hyper class from the dataset's own hyper block nf + nec: lg_hyper_reg<MT> takes up to
 // HR<MT>::RA = 8 MT - 2 columns (62 / 126)
 constexpr int HYPER_LDS_MAX = 138;   // lg_hyper's LDS block: (ms (ms + 1) + 3 ms) doubles < 160 KB
-// lg_hyper<2>: the timing-model + Fourier + augmented-row block it factors per likelihood
+// lg_hyper<2>: the timing-model + Fourier + augmented-row block X it factors per likelihood
 // (qx = ntm + nfourier + 1 rows) is at most EC_QX_MAX (its lower 16x16 tiles, at most
 // EC_TPW per wave, accumulate in MFMA registers); the epochs' couplings stream through LDS
 // EC_ECH epochs at a time
@@ -70,9 +70,16 @@ constexpr int EC_ECH = 32;
 static_assert(((EC_QX_MAX + 15) / 16) * ((EC_QX_MAX + 15) / 16 + 1) / 2 <= EC_TPW * (LBLK / 64),
               "lg_hyper<2> tiles per wave");
 // (force_lds: GST_DEBUG_LARGE_HYPER, the generic kernels: class 0, or 1 past HYPER_LDS_MAX)
+// Class 2 (epochs first) for every block past HYPER_LDS_MAX it can take, and for blocks past
+// lg_hyper_reg<8>'s 62 columns whose ECORR epochs outnumber X's rows (measured: mb, 20
+// Fourier + 60 epochs, 1.8-2.1x over lg_hyper_reg<16>; ecb, 20 + 24, 0.54-0.85x of
+// lg_hyper_reg<8>)
 __host__ __device__ constexpr int hyper_class(int hcols, int force_lds, int nec, int qx) {
-  return hcols > HYPER_LDS_MAX ? ((nec > 0 && qx <= EC_QX_MAX && !force_lds) ? 2 : 1)
-                               : (force_lds ? 0 : (hcols <= 8 * 8 - 2 ? 8 : (hcols <= 8 * 16 - 2 ? 16 : 0)));
+  return (nec > 0 && qx <= EC_QX_MAX && !force_lds &&
+          (hcols > HYPER_LDS_MAX || (hcols > 8 * 8 - 2 && nec >= qx)))
+             ? 2
+         : hcols > HYPER_LDS_MAX ? 1
+                                 : (force_lds ? 0 : (hcols <= 8 * 8 - 2 ? 8 : (hcols <= 8 * 16 - 2 ? 16 : 0)));
 }
 __host__ __device__ inline int hyper_class_of(const DevModel& md, int force_lds) {
   return hyper_class(md.nf + md.nec, force_lds, md.nec, md.ntm + md.nf + 1);

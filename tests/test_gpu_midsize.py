@@ -82,15 +82,14 @@ def test_register_hyper_matches_lds_hyper(pta):
 
 
 @pytest.mark.parametrize("name", ["ecb_beta_fixed", "ecb_uniform_fixed", "ecn_t_fixed",
-                                  "ecn_vvh17_fixed", "mb_beta_fixed", "mbn_vvh17_fixed",
-                                  "scaled_beta_fixed"])
+                                  "ecn_vvh17_fixed", "scaled_beta_fixed"])
 def test_register_hyper_matches_lds_hyper_ecorr(name):
     """lg_hyper_reg's ECORR and per-backend branches (phi^-1 of the ECORR columns from their
     backend's log10_ecorr, the ECORR log|phi| term, the b draw over ECORR columns) against
     lg_hyper on reference fixtures with 44 hyper columns (20 Fourier + 24 ECORR epochs:
-    lg_hyper_reg<8>) and 80 / 120 (mb: 20 + 60 ECORR; scaled: 60 components:
-    lg_hyper_reg<16>, two columns per lane); their parity with the reference itself is
-    test_gpu_parity.py's large-path replays."""
+    lg_hyper_reg<8>) and 120 (scaled: 60 components: lg_hyper_reg<16>, two columns per lane;
+    mb's 20 + 60 ECORR columns take lg_hyper<2>, the tests below); their parity with the
+    reference itself is test_gpu_parity.py's large-path replays."""
     if not torch.cuda.is_available():
         pytest.skip("needs a HIP device")
     from golden_io import load_ref, sweep_state
@@ -126,11 +125,13 @@ def test_register_hyper_matches_lds_hyper_ecorr(name):
         assert np.all(d <= 1e-8 * np.maximum(np.abs(b[k]), 1e-300) + 1e-300), (k, d.max())
 
 
-@pytest.mark.parametrize("name", ["ebig_beta_fixed", "ebig_t_fixed"])
+@pytest.mark.parametrize("name", ["ebig_beta_fixed", "ebig_t_fixed", "mb_beta_fixed",
+                                  "mbn_vvh17_fixed"])
 def test_epochs_first_hyper_matches_blocked_hyper(name):
-    """ebig (20 Fourier + 130 ECORR epochs, 14 timing-model columns): the epochs-first
-    elimination lg_hyper<2> (hyper class 2, the default) against the blocked global-memory one
-    lg_hyper<1> (GST_DEBUG_LARGE_HYPER) -- the b-marginalised likelihood at 256 states (prior
+    """ebig (20 Fourier + 130 ECORR epochs, 14 timing-model columns) and mb / mbn (20 + 60):
+    the epochs-first elimination lg_hyper<2> (hyper class 2, their default) against the
+    generic kernel GST_DEBUG_LARGE_HYPER forces (ebig: the blocked global-memory lg_hyper<1>;
+    mb: the LDS-resident lg_hyper<0>) -- the b-marginalised likelihood at 256 states (prior
     draws of x, the fixture's latents) within 1e-10 relative.  The two factor Sigma in
     different orders, so their Philox b draws are different (equally distributed) draws and
     the chains are compared with the reference instead: test_gpu_parity.py's large-path
@@ -165,17 +166,18 @@ def test_epochs_first_hyper_matches_blocked_hyper(name):
     assert r.max() <= 1e-10, r.max()
 
 
-def test_epochs_first_hyper_draws_match_blocked_hyper():
+@pytest.mark.parametrize("dataset", ["ebig", "mb"])
+def test_epochs_first_hyper_draws_match_blocked_hyper(dataset):
     """The two eliminations' Philox b draws are different draws of one law, so chains of the
-    same start through lg_hyper<2> and lg_hyper<1> must have the same marginal law at every
-    sweep (converged or not): 1024 ebig chains from prior draws, after 150 sweeps, every
+    same start through lg_hyper<2> and the generic kernel must have the same marginal law at
+    every sweep (converged or not): 1024 chains from prior draws, after 150 sweeps, every
     sampled parameter plus theta, nu and two b components, two-sample KS p > 1e-3."""
     if not torch.cuda.is_available():
         pytest.skip("needs a HIP device")
     import scipy.stats
     from golden_io import load_dataset
     from gibbs_student_t_amd.run_sims import MODELS
-    pta = load_dataset(dataset="ebig")
+    pta = load_dataset(dataset=dataset)
     C2, S2 = 1024, 150
     lo = np.array([p.pmin for p in pta.params])
     hi = np.array([p.pmax for p in pta.params])
