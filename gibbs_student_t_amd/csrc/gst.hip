@@ -552,7 +552,7 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
                   "red-noise / ECORR block elimination");
     // lg_hyper<2> (ECORR epochs eliminated first): its LDS vectors span the basis
     if (hc == 2 && (size_t)(2 * qx * (qx + 1) + nf + 2 * nec + 4 * mpl +
-                            gst::EC_ECH * (round_up(qx, 16) + 1)) * 8 > 160 * 1024)
+                            2 * gst::EC_ECH * (round_up(qx, 16) + 1)) * 8 > 160 * 1024)
       return fail("gst_model_set: large path: too many ECORR epochs for the LDS of their "
                   "elimination");
   }
@@ -596,10 +596,10 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
     cx->lds_hyper = lds_fits ? (size_t)(ms * (ms + 1) + h.nf + h.nec + 2 * ms) * 8 : 0;
     cx->lds_hyper_big = (size_t)(h.mp * (gst::TM_PW + 1) + gst::TM_PW + h.nf + h.nec + 2 * ms) * 8;
     // lg_hyper<2>: X and XB [qx][qx + 1], phi^-1 [nf + nec], four vectors of mp, a_e [nec],
-    // one chunk of couplings [EC_ECH][qxp] and its 1 / a_e
+    // two chunks of couplings [EC_ECH][qxp] and their 1 / a_e
     const int qx = h.ntm + h.nf + 1, qxp = round_up(qx, 16);
     cx->lds_hyper_ec = (size_t)(2 * qx * (qx + 1) + h.nf + h.nec + 4 * h.mp + h.nec +
-                                gst::EC_ECH * qxp + gst::EC_ECH) * 8;
+                                2 * gst::EC_ECH * qxp + 2 * gst::EC_ECH) * 8;
     cx->lds_btm = (size_t)(3 * h.ntm_pad + h.raug) * 8;
     HIP_OK(hipFuncSetAttribute((const void*)gst::lg_gram,
                                hipFuncAttributeMaxDynamicSharedMemorySize, gst::GRAM_LDS * 8));

@@ -172,6 +172,24 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
   return s;
 }
 
+// Three deterministic block sums (NW = 4 waves) behind one pair of barriers; red3: [3][4]
+__device__ __forceinline__ void block_sum3(double& a, double& b, double& c, double* red3) {
+  a = wave_sum(a);
+  b = wave_sum(b);
+  c = wave_sum(c);
+  const int wv = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    red3[wv] = a;
+    red3[4 + wv] = b;
+    red3[8 + wv] = c;
+  }
+  __syncthreads();
+  a = (red3[0] + red3[1]) + (red3[2] + red3[3]);
+  b = (red3[4] + red3[5]) + (red3[6] + red3[7]);
+  c = (red3[8] + red3[9]) + (red3[10] + red3[11]);
+}
+
 // MH variates of global step gs (0..19 white, 20..29 hyper) exactly as the persistent
 // kernel draws them (gst_kernel.hpp mh_variates): parameter, jump, log(u_acc), 10^(2 jump).
 __device__ __forceinline__ void mh_variate(const DevModel& md, const Rng& rng, const double* tp,
@@ -911,9 +929,9 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
   double* vv = ph + nf;                // [vlen] back-substitution accumulators / Delta
   double* wv_ = vv + vlen;             // [vlen] rhs
   double* aE = wv_ + vlen;             // EC: [nec] epoch pivots a_e
-  double* Ech = aE + nec;              // EC: [EC_ECH][qxp] couplings G_ex of a chunk of epochs
-  double* einv = Ech + EC_ECH * qxp;   // EC: [EC_ECH] 1 / a_e of the chunk
-  double* dl = einv + EC_ECH;          // EC: [mp] Delta (tape mode), internal order
+  double* Ech = aE + nec;              // EC: [2][EC_ECH][qxp] couplings G_ex, two chunks of epochs
+  double* einv = Ech + 2 * EC_ECH * qxp;   // EC: [2][EC_ECH] their 1 / a_e
+  double* dl = einv + 2 * EC_ECH;      // EC: [mp] Delta (tape mode), internal order
   double* vfull = dl + mp;             // EC: [mp] the b draw, internal order
   const double* Gg = a.s.G + (size_t)c * mp * mp;   // EC: the raw Gram (lower triangle)
   // EC: internal column of X's row i, and G at (r, q) from the lower triangle
@@ -937,6 +955,7 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
   // EC: the ECORR parameters XB, a_e and the epochs' likelihood terms (ecs) were made for
   __shared__ double eck[NBMAX];
   __shared__ double ecs[3];
+  __shared__ double red3[EC ? 12 : 1];
   __shared__ int ecvalid;
   if (EC && threadIdx.x == 0) ecvalid = 0;
   __shared__ double red[4];
@@ -996,11 +1015,13 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
         v4d acc[EC_TPW];
 #pragma unroll
         for (int h = 0; h < EC_TPW; ++h) acc[h] = v4d{0.0, 0.0, 0.0, 0.0};
-        for (int e0 = 0; e0 < nec; e0 += EC_ECH) {
+        // (two chunk buffers: chunk ch + 1 loads while chunk ch's MFMAs run, one barrier each)
+        auto load_chunk = [&](int e0, int bsel) {
           const int ne = nec - e0 < EC_ECH ? nec - e0 : EC_ECH;
+          double* E = Ech + bsel * EC_ECH * qxp;
           for (int t = tid; t < EC_ECH * qxp; t += LBLK) {
             const int ee = t / qxp, i = t - ee * qxp;
-            Ech[t] = (ee < ne && i < qx) ? Gl(K0 + nfr + e0 + ee, gx(i)) : 0.0;
+            E[t] = (ee < ne && i < qx) ? Gl(K0 + nfr + e0 + ee, gx(i)) : 0.0;
           }
           if (tid < EC_ECH) {
             double r = 0.0;
@@ -1010,17 +1031,24 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
               aE[e0 + tid] = ae;
               r = 1.0 / ae;
             }
-            einv[tid] = r;
+            einv[bsel * EC_ECH + tid] = r;
           }
-          __syncthreads();
+        };
+        const int nch = (nec + EC_ECH - 1) / EC_ECH;
+        load_chunk(0, 0);
+        __syncthreads();
+        for (int ch = 0; ch < nch; ++ch) {
+          if (ch + 1 < nch) load_chunk((ch + 1) * EC_ECH, (ch + 1) & 1);
+          const double* E = Ech + (ch & 1) * EC_ECH * qxp;
+          const double* ei = einv + (ch & 1) * EC_ECH;
 #pragma unroll
           for (int h = 0; h < EC_TPW; ++h) {
             if (!tin_[h]) continue;
 #pragma unroll
             for (int k4 = 0; k4 < EC_ECH / 4; ++k4) {
               const int kk = 4 * k4 + (lane >> 4);
-              const double av = Ech[kk * qxp + r0_[h] + (lane & 15)] * einv[kk];
-              const double bv = Ech[kk * qxp + c0_[h] + (lane & 15)];
+              const double av = E[kk * qxp + r0_[h] + (lane & 15)] * ei[kk];
+              const double bv = E[kk * qxp + c0_[h] + (lane & 15)];
               acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[h], 0, 0, 0);
             }
           }
@@ -1044,9 +1072,7 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
           lde += log(ae);
           qde += zr * zr * (1.0 / ae);
         }
-        lde = block_sum(lde, red);
-        qde = block_sum(qde, red);
-        fle = block_sum(fle, red);
+        block_sum3(lde, qde, fle, red3);
         if (tid == 0) {
           ecs[0] = lde;
           ecs[1] = qde;
@@ -1115,9 +1141,10 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
         ldx += log(akk);
         qdx += zr * zr * (1.0 / akk);
       }
-      ld = block_sum(ldx, red) + lde;
-      quad = block_sum(qdx, red) + qde;
-      fl = (block_sum(flx, red) != 0.0 || fle != 0.0) ? 1 : 0;
+      block_sum3(ldx, qdx, flx, red3);
+      ld = ldx + lde;
+      quad = qdx + qde;
+      fl = (flx != 0.0 || fle != 0.0) ? 1 : 0;
     } else if constexpr (BIG) {
       // blocked elimination of the hyper block (+ its augmented row) of S0 + diag(phi^-1):
       // G2 -> G3 (the block and the augmented row are contiguous there, raug = K0 + nf)
