@@ -1005,8 +1005,63 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
     double ld = 0.0, quad = 0.0;
     int fl = 0;
     if constexpr (EC) {
-      // XB = G_xx - sum_e G_xe G_ex / a_e: recomputed only when an ECORR parameter changed
-      // since the last factorisation (a proposal of log10_A or gamma reuses it)
+      // dense LDL^T of columns [k0, k1) of A, two columns per barrier: the trailing block
+      // (rows i, cols j <= i past k + 1: 32 row groups x 8 col groups) takes columns k and
+      // k + 1 at once, each thread forming column k + 1's updated entries c_i = A_i,k+1 -
+      // A_ik A_k+1,k / a_kk itself; column k + 1 itself is written back in the next round (no
+      // thread reads it there).  The trailing block covers every row and column past k1.
+      auto wback = [&](double* A, int kd) {   // column kd's update by column kd - 1
+        const double s10r = A[kd * SS + kd - 1] * (1.0 / A[(kd - 1) * SS + kd - 1]);
+        for (int i = kd + tid; i < qx; i += LBLK) A[i * SS + kd] -= A[i * SS + kd - 1] * s10r;
+      };
+      auto elim = [&](double* A, int k0, int k1) {
+        int kd = -1;
+        for (int k = k0; k < k1; k += 2) {
+          if (kd >= 0) wback(A, kd);
+          if (k + 1 < k1) {
+            const double r0 = 1.0 / A[k * SS + k];
+            const double s10r = A[(k + 1) * SS + k] * r0;
+            const double r1 = 1.0 / (A[(k + 1) * SS + k + 1] - A[(k + 1) * SS + k] * s10r);
+            const int i0 = k + 2 + (tid >> 3), j0 = k + 2 + (tid & 7);
+            for (int i = i0; i < qx; i += 32) {
+              const double sik = A[i * SS + k];
+              const double li0 = sik * r0, li1 = (A[i * SS + k + 1] - sik * s10r) * r1;
+              for (int j = j0; j <= i; j += 8) {
+                const double sjk = A[j * SS + k];
+                A[i * SS + j] -= li0 * sjk + li1 * (A[j * SS + k + 1] - sjk * s10r);
+              }
+            }
+            kd = k + 1;
+          } else {
+            const double r = 1.0 / A[k * SS + k];
+            const int i0 = k + 1 + (tid >> 3), j0 = k + 1 + (tid & 7);
+            for (int i = i0; i < qx; i += 32) {
+              const double lik = A[i * SS + k] * r;
+              for (int j = j0; j <= i; j += 8) A[i * SS + j] -= lik * A[j * SS + k];
+            }
+            kd = -1;
+          }
+          __syncthreads();
+        }
+        if (kd >= 0) {
+          wback(A, kd);
+          __syncthreads();
+        }
+      };
+      // per-thread partial sums of log a_kk, z_k^2 / a_kk and failed pivots over [k0, k1)
+      // (a pivot and its augmented-row entry are final once their column is eliminated)
+      auto colsums = [&](const double* A, int k0, int k1, double& l, double& qd, double& f) {
+        for (int k = k0 + tid; k < k1; k += LBLK) {
+          const double akk = A[k * SS + k], zr = A[nxd * SS + k];
+          f += !(akk > 0.0) ? 1.0 : 0.0;
+          l += log(akk);
+          qd += zr * zr * (1.0 / akk);
+        }
+      };
+      // XB = G_xx - sum_e G_xe G_ex / a_e + the timing-model prior, its timing-model columns
+      // eliminated: depends on the ECORR parameters only, so it is recomputed only when one
+      // changed since the last factorisation (a proposal of log10_A or gamma reuses it and
+      // factors the Fourier block alone)
       bool same = ecvalid != 0;
       for (int b = 0; b < md.nb; ++b) same = same && xget(q, md.ecorr_b[b]) == eck[b];
       if (!same) {
@@ -1060,10 +1115,16 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             const int i = r0_[h] + (lane >> 4) + 4 * g, j = c0_[h] + (lane & 15);
-            if (i < qx && j <= i) XB[i * SS + j] = Gg[(size_t)gx(i) * mp + gx(j)] - acc[h][g];
+            if (i < qx && j <= i) {
+              double v = Gg[(size_t)gx(i) * mp + gx(j)] - acc[h][g];
+              if (i == j && i < ntm) v = (v + md.tm_phiinv) + fsh;
+              XB[i * SS + j] = v;
+            }
           }
         }
-        // the epochs' pivots and augmented-row terms
+        __syncthreads();
+        elim(XB, 0, ntm);
+        // the epochs' and the timing model's pivots and augmented-row terms
         double lde = 0.0, qde = 0.0, fle = 0.0;
         for (int e = tid; e < nec; e += LBLK) {
           const double ae = aE[e];
@@ -1072,6 +1133,7 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
           lde += log(ae);
           qde += zr * zr * (1.0 / ae);
         }
+        colsums(XB, 0, ntm, lde, qde, fle);
         block_sum3(lde, qde, fle, red3);
         if (tid == 0) {
           ecs[0] = lde;
@@ -1082,65 +1144,19 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
         }
         __syncthreads();
       }
-      // X = XB + the timing-model and Fourier priors
+      // X = XB + the Fourier priors; its Fourier block (+ augmented row) factored per likelihood
       for (int t = tid; t < qx * qx; t += LBLK) {
         const int i = t / qx, j = t - i * qx;
         if (j > i) continue;
         double v = XB[i * SS + j];
-        if (i == j && i < nxd) v = (i < ntm) ? (v + md.tm_phiinv) + fsh : v + ph[i - ntm];
+        if (i == j && i >= ntm && i < nxd) v += ph[i - ntm];
         S[i * SS + j] = v;
       }
       const double lde = ecs[0], qde = ecs[1], fle = ecs[2];
       __syncthreads();
-      // dense LDL^T of X, two columns per barrier: the trailing block (rows i, cols j <= i
-      // past k + 1: 32 row groups x 8 col groups) takes columns k and k + 1 at once, each
-      // thread forming column k + 1's updated entries c_i = S_i,k+1 - S_ik S_k+1,k / a_kk
-      // itself; column k + 1 itself is written back in the next round (no thread reads it
-      // there).  The pivots' logs and the augmented row's terms after the loop, one column
-      // per thread (a pivot and its row entry are final once their column is eliminated).
-      auto wback = [&](int kd) {   // column kd's update by column kd - 1
-        const double s10r = S[kd * SS + kd - 1] * (1.0 / S[(kd - 1) * SS + kd - 1]);
-        for (int i = kd + tid; i < qx; i += LBLK) S[i * SS + kd] -= S[i * SS + kd - 1] * s10r;
-      };
-      int kd = -1;
-      for (int k = 0; k < nxd; k += 2) {
-        if (kd >= 0) wback(kd);
-        if (k + 1 < nxd) {
-          const double r0 = 1.0 / S[k * SS + k];
-          const double s10r = S[(k + 1) * SS + k] * r0;
-          const double r1 = 1.0 / (S[(k + 1) * SS + k + 1] - S[(k + 1) * SS + k] * s10r);
-          const int i0 = k + 2 + (tid >> 3), j0 = k + 2 + (tid & 7);
-          for (int i = i0; i < qx; i += 32) {
-            const double sik = S[i * SS + k];
-            const double li0 = sik * r0, li1 = (S[i * SS + k + 1] - sik * s10r) * r1;
-            for (int j = j0; j <= i; j += 8) {
-              const double sjk = S[j * SS + k];
-              S[i * SS + j] -= li0 * sjk + li1 * (S[j * SS + k + 1] - sjk * s10r);
-            }
-          }
-          kd = k + 1;
-        } else {
-          const double r = 1.0 / S[k * SS + k];
-          const int i0 = k + 1 + (tid >> 3), j0 = k + 1 + (tid & 7);
-          for (int i = i0; i < qx; i += 32) {
-            const double lik = S[i * SS + k] * r;
-            for (int j = j0; j <= i; j += 8) S[i * SS + j] -= lik * S[j * SS + k];
-          }
-          kd = -1;
-        }
-        __syncthreads();
-      }
-      if (kd >= 0) {
-        wback(kd);
-        __syncthreads();
-      }
+      elim(S, ntm, nxd);
       double ldx = 0.0, qdx = 0.0, flx = 0.0;
-      for (int k = tid; k < nxd; k += LBLK) {
-        const double akk = S[k * SS + k], zr = S[nxd * SS + k];
-        flx += !(akk > 0.0) ? 1.0 : 0.0;
-        ldx += log(akk);
-        qdx += zr * zr * (1.0 / akk);
-      }
+      colsums(S, ntm, nxd, ldx, qdx, flx);
       block_sum3(ldx, qdx, flx, red3);
       ld = ldx + lde;
       quad = qdx + qde;
