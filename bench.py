@@ -78,14 +78,42 @@ def persistent_shape(nf: int, ntm: int):
     return None
 
 
-def gram_mfma_flops(n: int, nf: int, ntm: int) -> float:
-    """fp64 MFMA flops the persistent kernel's Gram executes per chain-sweep: the lower
-    16x16 tiles of the padded augmented system, ceil(n / 4) k-steps of 16x16x4 each."""
+def gram_path_flops(n: int, nf: int, ntm: int, ncls: int, nflag: float) -> dict:
+    """Lane flops one chain-Gram executes on each persistent-kernel path (include/gst.h
+    gst_gram_counts).  The instance pads the system to 8 MT rows.
+      mfma:     the lower 16x16 tiles of the padded augmented system, ceil(n / 4) k-steps of
+                v_mfma_f64_16x16x4 (2 * 16 * 16 * 4 flops each) -- on the MFMA pipe;
+      low_rank: per class one FMA per lane per 8x8-cyclic slot (the class Grams), per flagged
+                TOA MT row-scaling multiplies + one FMA per slot (its rank-1 update) -- on
+                the VALU.
+    Executed (padded) work, not SURVEY.md 8d's algorithmic n (m+1)(m+2)."""
     sh = persistent_shape(nf, ntm)
     if sh is None:
-        return float("nan")
+        return {"mfma": float("nan"), "low_rank": float("nan")}
+    MT = sh[0]
     NT = (sh[2] + 1 + 15) // 16
-    return NT * (NT + 1) / 2 * ((n + 3) // 4) * 2 * 16 * 16 * 4
+    nsl = MT * (MT + 1) // 2
+    return {"mfma": NT * (NT + 1) / 2 * ((n + 3) // 4) * 2 * 16 * 16 * 4,
+            "low_rank": 64.0 * (ncls * 2 * nsl + nflag * (2 * nsl + MT))}
+
+
+def pmc_mfma(pf: str | None):
+    """MFMA work the committed PMC pass of the same command counted (rocprofv3 --pmc
+    SQ_INSTS_VALU_MFMA_MOPS_F64 (units of 512 flops) and SQ_VALU_MFMA_BUSY_CYCLES), per
+    chain-sweep, next to the fp64 VALU FMA count: what the Gram executes on which pipe."""
+    if not pf or not os.path.exists(pf):
+        return None
+    try:
+        pj = json.load(open(pf))
+        cs = float(pj["chains"]) * float(pj["sweeps"])
+        return {"source": os.path.relpath(pf, ROOT) + " (rocprofv3 --pmc pass of bench.py, "
+                          "not this run)",
+                "mfma_flop_per_chain_sweep": pj["SQ_INSTS_VALU_MFMA_MOPS_F64"] * 512.0 / cs,
+                "mfma_busy_cycles_per_chain_sweep": pj["SQ_VALU_MFMA_BUSY_CYCLES"] / cs,
+                "valu_fma_f64_insts_per_chain_sweep": pj["SQ_INSTS_VALU_FMA_F64"] / cs,
+                "valu_insts_per_chain_sweep": pj["SQ_INSTS_VALU"] / cs}
+    except (KeyError, ValueError, OSError):
+        return None
 
 
 def stage_costs(ns, S: int, seed: int, sweep0: int, chain0: int) -> dict:
@@ -103,12 +131,22 @@ def stage_costs(ns, S: int, seed: int, sweep0: int, chain0: int) -> dict:
     for name, mask in (("fixed", 0), ("toa_pass", toa), ("gram", _abi.STAGE_GRAM),
                        ("hyper", _abi.STAGE_HYPER)):
         t = []
+        ns.gram_counts(reset=True)
         for rep in range(2):        # the faster of two launches of each
             ns.sweep(S, seed=seed, sweep0=sweep0, chain0=chain0, mask=mask)
             ns.synchronize()
             t.append(ns.last_kernel_ms() / S)
         out[name] = min(t)
+        out[name + "_gram_paths"] = ns.gram_counts(reset=True)
     return out
+
+
+def noise_classes(pta) -> int:
+    """Noise classes of a dataset as gst_model_set forms them (equal error bar and backend;
+    0 past 8: the per-TOA white likelihood and the MFMA Gram)."""
+    err = np.asarray(pta._toaerrs)
+    keys = set(zip((err * err).tolist(), np.asarray(pta.bidx).tolist()))
+    return len(keys) if len(keys) <= 8 else 0
 
 
 def toa_pass_bytes(n: float) -> float:
@@ -577,10 +615,16 @@ def main():
         return time.perf_counter() - t0
 
     # ---- the timed region: exactly K sweeps, every sweep recorded
+    if not args.stub:
+        ns.gram_counts(reset=True)    # (synchronises: before the timed region's barrier)
     elapsed = timed(lambda: ns.sweep(K, records=rec, seed=args.seed, sweep0=W, chain0=c0))
     kernel_ms = ns.last_kernel_ms()
     ktimes = ns.kernel_times() if large else None
     status = ns.get_state()["status"]
+    # which Gram path each chain-sweep of the timed region took, and the flagged TOAs the
+    # low-rank path updates (z at the start of each sweep is the z its Gram uses)
+    gram_paths = None if args.stub else ns.gram_counts(reset=True)
+    zflag = float(rec["z"].sum(dim=-1).mean()) if "z" in rec else None
     del rec
     if large:
         ns.set_timing(False)
@@ -665,19 +709,23 @@ def main():
         # WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction) at 2048 chains: a rocprofv3
         # --pmc pass of this same command, stored under profiles/ -- NOT measured in this
         # run (counters need their own profiler pass); the newest profile is used
-        for pf in ("r5_pmc_config2.json", "r4_pmc_config2.json", "r3_pmc_config2.json"):
+        pmc2 = None
+        for pf in ("r6_pmc_config2.json", "r5_pmc_config2.json", "r4_pmc_config2.json",
+                   "r3_pmc_config2.json"):
             pmc = os.path.join(ROOT, "profiles", pf)
             if os.path.exists(pmc) and args.config == 2 and not args.stub:
                 try:
                     pj = json.load(open(pmc))
                     traffic = pj["hbm_bytes_per_chain_sweep"] * C * K
+                    pmc2 = pmc
                     traffic_src = (f"profiles/{pf}: rocprofv3 PMC pass of bench.py (not this "
                                    f"run), {pj['hbm_bytes_per_chain_sweep']:.0f} B per "
                                    "chain-sweep x chains x steps")
                     break
                 except Exception:
                     traffic = None
-        for pf in ("r5_pmc_config5.json", "r4_pmc_config5.json", "r3_pmc_config5.json"):
+        for pf in ("r6_pmc_config5.json", "r5_pmc_config5.json", "r4_pmc_config5.json",
+                   "r3_pmc_config5.json"):
             pmc5 = os.path.join(ROOT, "profiles", pf)
             if large and args.config == 5 and os.path.exists(pmc5):
                 try:   # HBM bytes per Gram launch (PMC passes of tools/run_large.py, same shape)
@@ -702,26 +750,46 @@ def main():
                            "sizes they are register / L2-resident, so this is NOT an HBM "
                            "rate (the kernel's HBM bytes: roofline.traffic, PMC)"}
             g_alg = n_eff * (m + 1) * (m + 2)
-            g_mf = gram_mfma_flops(int(n), pta0.nfourier, pta0.ntm)
-            h_exe = exe["gram"] + exe["tm_elim"] + exe["hyper_chol"]
+            pf = gram_path_flops(int(n), pta0.nfourier, pta0.ntm, noise_classes(pta0),
+                                 zflag if zflag is not None else 0.0)
+
+            def gram_exe(paths):
+                """(executed lane flops per chain-Gram, share of low-rank Grams) from the
+                path counts the kernel reported (gst_gram_counts)."""
+                tot = paths["low_rank"] + paths["mfma"]
+                if tot <= 0:
+                    return float("nan"), float("nan")
+                f_lr = paths["low_rank"] / tot
+                return f_lr * pf["low_rank"] + (1 - f_lr) * pf["mfma"], f_lr
+
+            g_exe, g_lr = gram_exe(stage_ms["gram_gram_paths"])
+            h_exe = g_exe + exe["tm_elim"] + exe["hyper_chol"]
             h_fix = g_alg + 12 * m ** 3 / 3
             stage_rep = {
                 "source": "stage-masked launches of this run (HIP events), fixed cost "
-                          f"{fx * 1e3:.1f} us/sweep subtracted",
+                          f"{fx * 1e3:.1f} us/sweep subtracted; Gram paths counted by the "
+                          "kernel (gst_gram_counts)",
                 "gram": {"ms_per_sweep": t_gram,
+                         "paths": stage_ms["gram_gram_paths"],
+                         "low_rank_share": g_lr,
+                         "executed_lane_flop_per_chain_gram": {
+                             "low_rank_valu": pf["low_rank"], "mfma": pf["mfma"],
+                             "flagged_toas_mean": zflag},
+                         "tflops_executed": (g_exe + exe["tm_elim"]) * C / (t_gram * 1e-3) / 1e12,
                          "tflops_algorithmic": (g_alg + exe["tm_elim"]) * C / (t_gram * 1e-3) / 1e12,
-                         "mfma_tflops_executed": g_mf * C / (t_gram * 1e-3) / 1e12,
-                         "what": "Gram T^T N^-1 [T|r] (fp64 MFMA 16x16x4) + timing-model "
-                                 "elimination"},
+                         "pipe": ("VALU (low-rank: class Grams + rank-1 updates)"
+                                  if g_lr > 0.5 else "fp64 MFMA 16x16x4"),
+                         "what": "Gram T^T N^-1 [T|r] + timing-model elimination; low-rank "
+                                 "path on the VALU, n-TOA path on the fp64 MFMA (DESIGN.md 4)"},
                 "gram_cholesky": {"ms_per_sweep": t_hyp,
                                   "tflops_executed": h_exe * C / (t_hyp * 1e-3) / 1e12,
                                   "tflops_fixed_formula": h_fix * C / (t_hyp * 1e-3) / 1e12,
                                   "what": "whole red-noise block: Gram + 11 likelihood "
-                                          "factorisations"},
+                                          "factorisations (VALU: register-resident LDL^T)"},
             }
             for v in stage_rep.values():
                 if isinstance(v, dict):
-                    for k2 in [k for k in v if k.startswith(("tflops", "mfma_tflops"))]:
+                    for k2 in [k for k in v if k.startswith("tflops")]:
                         v[k2.replace("tflops", "frac")] = v[k2] / FP64_PEAK_TFLOPS
         ess_ps, reason = None, None
         if ess is None:
@@ -782,9 +850,10 @@ def main():
                                    "since_start_draws": int(s_vec[2])}),
             "kernel_ms": kernel_ms,
             # the persistent kernel is bound by VALU issue and the latency of the
-            # factorisations' step-to-step LDS hand-offs (PMC: MFMA busy ~11%, VALU ~57% of
-            # issue slots); its roofline is the fp64 peak, which MFMA
-            # and VALU share on MI355X.  The large path's Gram is MFMA-bound.
+            # factorisations' step-to-step LDS hand-offs (on config 2 its
+            # Gram is the low-rank VALU update, so the PMC counts ~no MFMA work: roofline
+            # ["gram_paths"] and ["mfma_pmc"]); its roofline is the fp64 peak, which MFMA and
+            # VALU share on MI355X.  The large path's Gram is MFMA-bound.
             "roofline": {"bound": "mfma" if large else "valu-latency",
                          "peak_kind": "fp64 dense (MFMA = VALU rate on MI355X)",
                          "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
@@ -795,6 +864,12 @@ def main():
                          "algorithmic_flop_per_chain_sweep": algorithmic_flops(n_eff, m),
                          "executed_flop_per_chain_sweep": exe,
                          "per_toa_pass": toa,
+                         "gram_paths": (None if gram_paths is None else
+                                        dict(gram_paths, what="chain-Grams of the timed "
+                                             "region by path (gst_gram_counts): persistent "
+                                             "low-rank (VALU) / persistent MFMA / large-path "
+                                             "MFMA")),
+                         "mfma_pmc": pmc_mfma(pmc2) if not large else None,
                          "stages": stage_rep},
             "cpu_baseline": cpu,
         }

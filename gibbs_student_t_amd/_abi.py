@@ -37,15 +37,17 @@ def floor_draws(status):
 PATHS = {"auto": PATH_AUTO, "persistent": PATH_PERSISTENT, "large": PATH_LARGE}
 KERNEL_KINDS = ("record", "white", "gram", "tmelim", "hyper", "btm", "tb", "toa")
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 EXPORTS = ("gst_version", "gst_tape_stride", "gst_last_error", "gst_ctx_create",
            "gst_ctx_destroy", "gst_model_set", "gst_model_set_batch", "gst_model_info",
            "gst_sweep", "gst_set_path", "gst_get_path", "gst_set_waves", "gst_set_debug", "gst_set_timing", "gst_kernel_times", "gst_eval_lnlike", "gst_sync",
-           "gst_last_sweep_ms", "gst_debug_stamps", "gst_simulate")
+           "gst_last_sweep_ms", "gst_debug_stamps", "gst_simulate",
+           # ABI 6
+           "gst_gram_counts", "gst_debug_variates")
 
 # diagnostics that older builds (A/B timing of library variants) may lack; calling one on
 # such a build raises AttributeError
-OPTIONAL = ("gst_set_debug",)
+OPTIONAL = ("gst_set_debug", "gst_gram_counts", "gst_debug_variates")
 
 _P = ct.POINTER
 _D = _P(ct.c_double)
@@ -155,6 +157,11 @@ def load(path: str | None = None):
     lib.gst_last_sweep_ms.argtypes = [ct.c_void_p, _P(ct.c_double)]
     lib.gst_debug_stamps.argtypes = [ct.c_void_p, ct.c_void_p]
     lib.gst_simulate.argtypes = [_P(SimDesc), ct.c_void_p]
+    if hasattr(lib, "gst_gram_counts"):
+        lib.gst_gram_counts.argtypes = [ct.c_void_p, _P(ct.c_longlong), ct.c_int]
+    if hasattr(lib, "gst_debug_variates"):
+        lib.gst_debug_variates.argtypes = [ct.c_int, ct.c_double, ct.c_double, ct.c_longlong,
+                                           ct.c_ulonglong, ct.c_uint, ct.c_void_p, ct.c_void_p]
     for name in EXPORTS:
         if name != "gst_version" and hasattr(lib, name):
             getattr(lib, name).restype = ct.c_int

@@ -50,6 +50,8 @@ struct Ctx {
   int path = GST_PATH_PERSISTENT;  // chosen by gst_model_set
   int waves = GST_WAVES_AUTO;      // gst_set_waves
   int debug = 0;                   // gst_set_debug
+  unsigned long long* gram_cnt = nullptr;  // persistent path: [2] Grams by path (gst_gram_counts)
+  unsigned long long gram_large = 0;       // large path: chain Grams launched (lg_gram*)
   std::vector<void*> allocs;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
@@ -144,6 +146,38 @@ const Shape* shape_for(int nf, int ntm, bool gen = false) {
 
 int round_up(int a, int b) { return (a + b - 1) / b * b; }
 
+// gst_debug_variates: the kernel's own samplers, one draw (kind 0, 1) or four (kind 2) per
+// thread, Philox keyed by (seed, chain 0xFFFFFFF0, sweep = call, index, TAG_DEBUG).
+constexpr uint32_t TAG_DEBUG = 14u << 24;
+__global__ void __launch_bounds__(256) debug_variates_kernel(int kind, double a, double b,
+                                                             long long n, unsigned long long seed,
+                                                             unsigned call, double* out) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  gst::Rng rng;
+  rng.k0 = (uint32_t)(seed & 0xffffffffull);
+  rng.k1 = (uint32_t)(seed >> 32);
+  rng.chain = 0xFFFFFFF0u;
+  rng.sweep = call;
+  if (kind == 0) {              // gamma_mt(a): the theta stage's Gamma
+    if (i < n) out[i] = gst::gamma_mt(a, rng, (uint32_t)i, TAG_DEBUG);
+  } else if (kind == 1) {       // the theta stage's Beta(a, b) = Ga / (Ga + Gb)
+    if (i < n) {
+      const double ga = gst::gamma_mt(a, rng, (uint32_t)(2 * i), TAG_DEBUG);
+      const double gb = gst::gamma_mt(b, rng, (uint32_t)(2 * i + 1), TAG_DEBUG);
+      out[i] = ga / (ga + gb);
+    }
+  } else {                      // gamma_mt_slots<4>: the alpha stage's interleaved Gammas
+    const long long w = i >> 6, l = i & 63;
+    if (256 * w < n) {
+      const double sh[4] = {a, a, a, a};
+      double g[4];
+      gst::gamma_mt_slots<4>(sh, 0xFu, rng, (uint32_t)(256 * w + l), TAG_DEBUG, g);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) out[256 * w + 64 * s + l] = g[s];
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -172,6 +206,8 @@ int gst_ctx_create(int device, void** ctx) {
   HIP_OK(hipEventCreate(&cx->ev0));
   HIP_OK(hipEventCreate(&cx->ev1));
   HIP_OK(hipMalloc(&cx->prog, 256));   // fair_prio's launch-wide sweep counter
+  HIP_OK(hipMalloc(&cx->gram_cnt, 2 * sizeof(unsigned long long)));
+  HIP_OK(hipMemset(cx->gram_cnt, 0, 2 * sizeof(unsigned long long)));
   *ctx = cx;
   return 0;
 }
@@ -182,6 +218,7 @@ int gst_ctx_destroy(void* ctx) {
   (void)hipSetDevice(cx->device);
   free_model(cx);
   if (cx->prog) (void)hipFree(cx->prog);
+  if (cx->gram_cnt) (void)hipFree(cx->gram_cnt);
   for (hipEvent_t e : cx->evpool) (void)hipEventDestroy(e);
   if (cx->ev0) (void)hipEventDestroy(cx->ev0);
   if (cx->ev1) (void)hipEventDestroy(cx->ev1);
@@ -440,6 +477,18 @@ static int pack_dataset(Ctx* cx, const gst_model_desc* d, gst::DevModel& md, int
   return 0;
 }
 
+// ECORR epochs are disjoint when no TOA has a nonzero entry in two of the last n_ecorr
+// columns of T (lg_hyper<2>'s elimination takes the ECORR block of T^T N^-1 T as diagonal)
+static bool ecorr_disjoint(const gst_model_desc* d) {
+  const int m = d->m, nec = d->n_ecorr;
+  for (int t = 0; t < d->n; ++t) {
+    int nz = 0;
+    for (int j = m - nec; j < m; ++j) nz += d->T[(size_t)t * m + j] != 0.0;
+    if (nz > 1) return false;
+  }
+  return true;
+}
+
 static int check_desc(const gst_model_desc* d) {
   const int n = d->n, m = d->m, nf = d->nfourier, ntm = d->ntm, P = d->nparams;
   const int nec = d->n_ecorr, nb = d->nbackend > 0 ? d->nbackend : 1;
@@ -514,6 +563,8 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
   }
   const gst_model_desc* d = &descs[0];
   const int nf = d->nfourier, ntm = d->ntm, m = d->m, nec = d->n_ecorr;
+  bool disjoint = true;   // the batch's datasets all: one hyper class per batch structure
+  for (int i = 0; i < nd && nec > 0; ++i) disjoint = disjoint && ecorr_disjoint(&descs[i]);
   const bool gen = !classic(d) && general_fits(d);
   const Shape* sh = shape_for(nf + (gen ? nec : 0), ntm, gen);
   const int MT = sh ? sh->MT : 0, K0 = sh ? sh->K0 : 0;
@@ -545,7 +596,7 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
     // Fourier block are eliminated first (lg_hyper<2>), other blocks are factored in global
     // memory (lg_hyper<1>), whose LDS holds a 16-column panel of all mp rows plus three vectors
     const int ms = nf + nec + 1, mpl = round_up(round_up(ntm > 0 ? ntm : 1, 16) + nf + nec + 1, 16);
-    const int hc = gst::hyper_class(nf + nec, 0, nec, ntm + nf + 1), qx = ntm + nf + 1;
+    const int hc = gst::hyper_class(nf + nec, 0, nec, ntm + nf + 1, disjoint ? 1 : 0), qx = ntm + nf + 1;
     if (hc == 1 &&
         (size_t)(mpl * (gst::TM_PW + 1) + gst::TM_PW + nf + nec + 2 * ms) * 8 > 160 * 1024)
       return fail("gst_model_set: large path: basis too large for the LDS panel of the "
@@ -561,12 +612,14 @@ int gst_model_set_batch(void* ctx, const gst_model_desc* descs, int nd) {
   const int ntm_pad = path == GST_PATH_LARGE ? round_up(ntm > 0 ? ntm : 1, 16) : 8 * K0;
   const int raug_pack = path == GST_PATH_LARGE ? ntm_pad + nf + nec : raug;
   std::vector<gst::DevModel> hmd(nd);
-  for (int i = 0; i < nd; ++i)
+  for (int i = 0; i < nd; ++i) {
     if (pack_dataset(cx, &descs[i], hmd[i], ntm_pad, raug_pack,
                      path == GST_PATH_PERSISTENT ? MT : 0)) {
       free_model(cx);
       return -1;
     }
+    hmd[i].ec_disjoint = disjoint ? 1 : 0;
+  }
   void* ptr;
   if (upload(cx, hmd.data(), hmd.size() * sizeof(gst::DevModel), &ptr)) return -1;
   cx->dmd = (gst::DevModel*)ptr;
@@ -718,6 +771,11 @@ static int launch_hyper(Ctx* cx, gst::LArgs& a, const bool (&hcls)[5], dim3 g8, 
     LG_LAUNCH(GST_K_HYPER, gst::lg_hyper<0>, g_chain, b_chain, cx->lds_hyper);
   }
   if (hcls[3]) {
+    // (a class-2 model forced here by GST_DEBUG_LARGE_HYPER may have a block whose panel
+    // does not fit the LDS: refuse it rather than fail at launch)
+    if (cx->lds_hyper_big > 160 * 1024)
+      return fail("gst: GST_DEBUG_LARGE_HYPER: this model's red-noise / ECORR block is too "
+                  "large for the blocked elimination's LDS panel (lg_hyper<1>)");
     a.kclass = 1;
     LG_LAUNCH(GST_K_HYPER, gst::lg_hyper<1>, g_chain, b_chain, cx->lds_hyper_big);
   }
@@ -802,6 +860,7 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
       }
       HIP_OK(hipGetLastError());
       if (ev_mark(cx, GST_K_GRAM, st, false)) return -1;
+      if (!eval_only) cx->gram_large += (unsigned long long)C;
       LG_LAUNCH(GST_K_TMELIM, gst::lg_tmelim, g_chain, b_chain, cx->lds_tm);
       if (!(mask & GST_STAGE_GRAM)) {   // timing diagnostic: Gram + TM elimination only
         if (launch_hyper(cx, a, hcls, g_hr8, b_hr8, g_hr16, b_hr16, g_chain, b_chain, st))
@@ -853,7 +912,7 @@ static int launch(Ctx* cx, const gst_state* s, const gst_records* r, const gst_t
     return fail("gst: the model has several datasets: state.dataset must be set");
   gst::DevState ds{s->x,     s->b,  s->z,      s->alpha,   s->pout, s->theta,
                    s->nu,    s->status, s->dataset, cx->nmax, cx->nd, nullptr, nullptr,
-                   cx->debug};
+                   cx->debug, eval_only ? nullptr : cx->gram_cnt};
   gst::DevRec dr{};
   if (r) dr = gst::DevRec{r->x, r->b, r->z, r->alpha, r->pout, r->theta, r->nu, r->nrec};
   else record_every = 0;
@@ -871,7 +930,7 @@ static int launch(Ctx* cx, const gst_state* s, const gst_records* r, const gst_t
   }
   // two waves per chain when every chain would otherwise leave a SIMD idle
   // (not for the general white-noise model: its instances run one wave per chain)
-  if (cx->gen && cx->waves == GST_WAVES_TWO)
+  if (cx->gen && cx->waves == GST_WAVES_TWO && !tape && !eval_only)
     return fail("gst: two waves per chain are not built for the general white-noise model "
                 "(per-backend white noise / ECORR); use GST_WAVES_AUTO or GST_WAVES_ONE");
   const bool pair = !cx->gen && !tape && !eval_only && !(mask & GST_STAGE_GRAM) &&
@@ -1047,6 +1106,38 @@ int gst_simulate(const gst_sim_desc* d, void* stream) {
   a.r_clean = d->residuals_clean;
   hipLaunchKernelGGL(gst::gst_simulate_kernel, dim3(d->ndatasets), dim3(gst::SIM_BLOCK), 0,
                      (hipStream_t)stream, a);
+  HIP_OK(hipGetLastError());
+  return 0;
+}
+
+int gst_gram_counts(void* ctx, long long* counts, int reset) {
+  Ctx* cx = static_cast<Ctx*>(ctx);
+  if (!cx || !counts) return fail("gst_gram_counts: null argument");
+  HIP_OK(hipSetDevice(cx->device));
+  HIP_OK(hipDeviceSynchronize());
+  unsigned long long h[2] = {0ull, 0ull};
+  HIP_OK(hipMemcpy(h, cx->gram_cnt, sizeof h, hipMemcpyDeviceToHost));
+  counts[0] = (long long)h[0];
+  counts[1] = (long long)h[1];
+  counts[2] = (long long)cx->gram_large;
+  if (reset) {
+    HIP_OK(hipMemset(cx->gram_cnt, 0, sizeof h));
+    cx->gram_large = 0;
+  }
+  return 0;
+}
+
+int gst_debug_variates(int kind, double a, double b, long long n, unsigned long long seed,
+                       unsigned call, double* out, void* stream) {
+  if (!out || n < 0) return fail("gst_debug_variates: bad argument");
+  if (kind < 0 || kind > 2) return fail("gst_debug_variates: kind must be 0, 1 or 2");
+  if (!(a > 0.0) || (kind == 1 && !(b > 0.0))) return fail("gst_debug_variates: shapes must be > 0");
+  if ((kind == 2 && n % 256) || n > (1ll << 31))
+    return fail("gst_debug_variates: n must be <= 2^31 (kind 2: a multiple of 256)");
+  if (n == 0) return 0;
+  const long long threads = kind == 2 ? n / 4 : n;
+  hipLaunchKernelGGL(debug_variates_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, kind, a, b, n, seed, call, out);
   HIP_OK(hipGetLastError());
   return 0;
 }

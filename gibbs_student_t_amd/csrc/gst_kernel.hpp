@@ -64,6 +64,7 @@ constexpr int KP_MIN = 4;
 // gram_and_tm's low-rank Gram takes sweeps with at most LR_MAX flagged TOAs (z = 1): past
 // that the n-TOA MFMA Gram is cheaper, and the class Grams' share that cancels grows
 constexpr int LR_MAX = 32;
+constexpr double LR_ALPHA_MAX = 0x1p20;   // ... and alpha_t <= 2^20 on every flagged TOA
 // the largest TOA-slot count whose two-chains-per-SIMD build the host picks (wider shapes
 // run one chain per SIMD)
 constexpr int OCC2_NS_MAX = 8;
@@ -125,6 +126,7 @@ struct DevModel {
   const int* bk;            // [npad] backend of each TOA (null when nb == 1)
   int efac_b[NBMAX], equad_b[NBMAX], ecorr_b[NBMAX];
   int nec;
+  int ec_disjoint;          // every TOA in at most one ECORR column (the batch's datasets all)
   const int* ecb;           // [nec] backend of each ECORR column
   double ec_count[NBMAX];   // ECORR columns per backend
   double sig_h, sig_w;
@@ -147,6 +149,7 @@ struct DevState {
   unsigned long long* prog;  // chain-sweeps started in this launch (two chains per SIMD), or
                              // null: see fair_prio
   int debug;                 // GST_DEBUG_* flags (gst_set_debug)
+  unsigned long long* gram_cnt;  // [2] Grams computed: low-rank, MFMA (gst_gram_counts), or null
 };
 struct DevRec {
   double *x, *b, *z, *alpha, *pout, *theta, *nu;
@@ -1017,6 +1020,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
   __shared__ double xpo[PAIR ? NS : 1][PAIR ? 64 : 1], xal[PAIR ? NS : 1][PAIR ? 64 : 1];
   __shared__ double xyv[PAIR ? NS : 1][PAIR ? 64 : 1];   // pair mode: the drawer's y = r - T b
   __shared__ unsigned long long xzm[PAIR ? NS : 1];
+  __shared__ unsigned gcnt[WPB][2];            // Grams by path (gst_gram_counts)
 
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1130,6 +1134,13 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       return md.sig2[64 * s + lane];
   };
   int status = 0, nfloor = 0;   // nfloor: b draws at the SVD noise floor in this launch
+  // Grams computed in this launch by path (gst_gram_counts): low-rank (class Grams + rank-1
+  // updates on the VALU) and n-TOA fp64 MFMA, counted in LDS (registers held across the sweep
+  // loop raised the two-chains-per-SIMD build's spill by 32 B/lane)
+  if (lane == 0) {
+    gcnt[wv][0] = 0u;
+    gcnt[wv][1] = 0u;
+  }
   lds_order();
 
   // y = r - T b (gibbs.py:213,237,272): 8 columns x NS TOA slots of loads in flight
@@ -1398,10 +1409,20 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
     // with the per-class Grams G_k of the dataset (DevModel::Gcls) -- the same T^T N^-1 [T|r]
     // (gibbs.py:302-304) at a cost of the class terms plus one rank-1 update per flagged TOA
     // instead of the MFMA Gram over all n TOAs (config 2: ~7 flagged of 130).
+    // Taken only while every flagged TOA's alpha is at most LR_ALPHA_MAX: the rank-1 terms
+    // subtract c_k (1 - 1 / alpha_t) of a class Gram's share, so a direction fixed by flagged
+    // TOAs alone keeps an absolute error ~eps c_k |row|^2 against its true c_k |row|^2 / alpha_t
+    // (relative ~eps alpha_t); past the bound (vvh17's fixed alpha = 1e10) the MFMA Gram runs.
     int nout = 0;
+    bool big = false;
 #pragma unroll
-    for (int s = 0; s < NS; ++s) nout += __popcll(__ballot(((zb & vmask) >> s) & 1u));
-    if (md.Gcls && nout <= LR_MAX && !(st.debug & DEBUG_MFMA_GRAM)) {
+    for (int s = 0; s < NS; ++s) {
+      nout += __popcll(__ballot(((zb & vmask) >> s) & 1u));
+      big = big || ((((zb & vmask) >> s) & 1u) && al[s] > LR_ALPHA_MAX);
+    }
+    if (md.Gcls && nout <= LR_MAX && !(st.debug & DEBUG_MFMA_GRAM) && __ballot(big) == 0ull) {
+      __hip_atomic_fetch_add(&gcnt[wv][0], lane == 0 ? 1u : 0u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WAVEFRONT);
 #pragma unroll
       for (int i = 0; i < SL(MT, 0); ++i) L[i] = 0.0;
 #pragma unroll 1
@@ -1449,6 +1470,8 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       }
       GST_SUB_END(9)
     } else {
+    __hip_atomic_fetch_add(&gcnt[wv][1], lane == 0 ? 1u : 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WAVEFRONT);
     if constexpr (PAIR) {
     // Two waves per chain (PAIR): wave 0 computes the
     // even Gram tiles, wave 1 the odd ones (each its own MFMA pipe), then the tiles are swapped
@@ -2547,10 +2570,17 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
       prow[t] = po[s];
     }
   }
+  lds_order();   // the Gram counters' LDS adds precede their read
   if (lane == 0) {
     st.theta[c] = theta;
     st.nu[c] = nu;
     if (st.status) st.status[c] = (st.status[c] | status) + nfloor * STATUS_FLOOR_COUNT;
+    if (st.gram_cnt) {
+      __hip_atomic_fetch_add(st.gram_cnt, (unsigned long long)gcnt[wv][0], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(st.gram_cnt + 1, (unsigned long long)gcnt[wv][1],
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 

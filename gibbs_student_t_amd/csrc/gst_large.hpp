@@ -74,15 +74,19 @@ static_assert(((EC_QX_MAX + 15) / 16) * ((EC_QX_MAX + 15) / 16 + 1) / 2 <= EC_TP
 // lg_hyper_reg<8>'s 62 columns whose ECORR epochs outnumber X's rows (measured: mb, 20
 // Fourier + 60 epochs, 1.8-2.1x over lg_hyper_reg<16>; ecb, 20 + 24, 0.54-0.85x of
 // lg_hyper_reg<8>)
-__host__ __device__ constexpr int hyper_class(int hcols, int force_lds, int nec, int qx) {
-  return (nec > 0 && qx <= EC_QX_MAX && !force_lds &&
+// Class 2 needs disjoint epochs (each TOA in at most one ECORR column: the ECORR block of
+// T^T N^-1 T is then diagonal, which its elimination assumes); gst_model_set checks the basis
+// (DevModel::ec_disjoint) and other ECORR bases take class 1 / the register kernels.
+__host__ __device__ constexpr int hyper_class(int hcols, int force_lds, int nec, int qx,
+                                              int disjoint = 1) {
+  return (nec > 0 && disjoint && qx <= EC_QX_MAX && !force_lds &&
           (hcols > HYPER_LDS_MAX || (hcols > 8 * 8 - 2 && nec >= qx)))
              ? 2
          : hcols > HYPER_LDS_MAX ? 1
                                  : (force_lds ? 0 : (hcols <= 8 * 8 - 2 ? 8 : (hcols <= 8 * 16 - 2 ? 16 : 0)));
 }
 __host__ __device__ inline int hyper_class_of(const DevModel& md, int force_lds) {
-  return hyper_class(md.nf + md.nec, force_lds, md.nec, md.ntm + md.nf + 1);
+  return hyper_class(md.nf + md.nec, force_lds, md.nec, md.ntm + md.nf + 1, md.ec_disjoint);
 }
 constexpr int GRAM_WAVES = 8;  // chains per gram workgroup
 #ifndef GST_TM_PW

@@ -286,6 +286,15 @@ class NativeSampler:
         _abi.check(self.lib, self.lib.gst_kernel_times(self.ctx, ms, nl, k), "gst_kernel_times")
         return {name: (ms[i], nl[i]) for i, name in enumerate(_abi.KERNEL_KINDS)}
 
+    def gram_counts(self, reset: bool = True):
+        """Grams computed since the last reset, by path (include/gst.h gst_gram_counts):
+        {"low_rank": persistent low-rank (VALU), "mfma": persistent fp64 MFMA,
+        "large_mfma": large path fp64 MFMA} in chain-Grams; synchronises the device."""
+        v = (ct.c_longlong * 3)()
+        _abi.check(self.lib, self.lib.gst_gram_counts(self.ctx, v, int(bool(reset))),
+                   "gst_gram_counts")
+        return {"low_rank": int(v[0]), "mfma": int(v[1]), "large_mfma": int(v[2])}
+
     def close(self):
         if getattr(self, "ctx", None):
             self.lib.gst_ctx_destroy(self.ctx)
@@ -317,3 +326,20 @@ def pack_tape(ref_tape: dict, sweeps, n: int, m: int, stride: int, nst: int | No
         row[o + m + 1 + nst:o + m + 1 + nst + n] = ref_tape["gamma"][i]
         row[o + m + 1 + 2 * nst] = ref_tape["df_u"][i]
     return rows
+
+
+def debug_variates(kind: str, a: float, n: int, b: float = 1.0, seed: int = 1, call: int = 0,
+                   device: int = 0):
+    """The kernel's own samplers (include/gst.h gst_debug_variates) -> float64 device tensor:
+    kind "gamma" (gamma_mt), "beta" (the theta stage's two-gamma Beta), "gamma_slots" (the
+    alpha stage's gamma_mt_slots<4>; n a multiple of 256)."""
+    torch = _torch()
+    lib = _abi.load()
+    k = {"gamma": 0, "beta": 1, "gamma_slots": 2}[kind]
+    out = torch.empty(int(n), dtype=torch.float64, device=f"cuda:{device}")
+    with torch.cuda.device(device):
+        st = torch.cuda.current_stream().cuda_stream
+        rc = lib.gst_debug_variates(k, float(a), float(b), int(n), int(seed), int(call),
+                                    ct.c_void_p(out.data_ptr()), ct.c_void_p(st))
+    _abi.check(lib, rc, "gst_debug_variates")
+    return out

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GST_ABI_VERSION 5
+#define GST_ABI_VERSION 6
 
 /* Outlier model kind: Gibbs(model=...) (gibbs.py:9,32,187-226). */
 enum gst_outlier_model {
@@ -105,7 +105,11 @@ typedef struct gst_model_desc {
   const int* ecorr_idx;    /* nbackend: each backend's log10_ecorr, -1 = none (NULL: none) */
   int n_ecorr;             /* ECORR basis columns: the LAST n_ecorr columns of T, prior
                               variance 10^(2 log10_ecorr) of their backend; m = nfourier +
-                              ntm + n_ecorr */
+                              ntm + n_ecorr.  Epochs are normally disjoint (each TOA in at
+                              most one ECORR column, enterprise's quantised basis); the large
+                              path then eliminates them first, and only then:
+                              gst_model_set checks the basis, and a batch with any TOA in two
+                              ECORR columns takes the general elimination (ABI 6) */
   const int* ecorr_backend;/* n_ecorr: backend of each ECORR column */
 } gst_model_desc;
 
@@ -232,7 +236,8 @@ int gst_get_path(void* ctx, int* path);
  * chain's draws are bitwise those of the one-wave kernel.  GST_WAVES_ONE / GST_WAVES_TWO
  * force either kernel for every sampling launch (tape-mode and gst_eval_lnlike launches
  * always run one wave per chain).  The general white-noise model has no two-wave kernel: AUTO
- * runs it on one wave, and a sweep with GST_WAVES_TWO set fails. */
+ * runs it on one wave, and a sampling launch (gst_sweep without a tape) with GST_WAVES_TWO
+ * set fails; its tape-mode and gst_eval_lnlike launches run one wave as for every model. */
 enum gst_waves { GST_WAVES_AUTO = 0, GST_WAVES_ONE = 1, GST_WAVES_TWO = 2 };
 int gst_set_waves(void* ctx, int waves);
 
@@ -250,6 +255,11 @@ int gst_set_waves(void* ctx, int waves);
  * Test switches (the defaults are the faster kernels). */
 /* GST_DEBUG_EXACT_BDRAW: every b draw is the exact draw from Sigma, also beyond fp64
  * resolution (no SVD noise floor, see gst_sweep). */
+/* The floor gate's pivot order: the timing-model-first LDL^T (real columns) on the
+ * persistent path and the large path's classes 0 / 1 and register kernels; the large path's
+ * class 2 (ECORR epochs eliminated first, lg_hyper<2>) gates on the pivots of its own order
+ * [ECORR | TM | Fourier].  Pivot ratios depend on the order, so near the 2^-52 gate the two
+ * orders can decide a draw differently (both draw exactly from Sigma or Sigma + f I). */
 /* GST_DEBUG_MFMA_GRAM (ABI 5): the persistent kernel computes every Gram on the MFMA path,
  * never the low-rank one (datasets of <= 8 noise classes, at most 32 flagged TOAs: the
  * per-class Grams plus one rank-1 update per flagged TOA); the two agree
@@ -281,6 +291,27 @@ int gst_debug_stamps(void* ctx, unsigned long long* dev_buf);
 
 /* Kernel-level timing of the last gst_sweep on its stream (hipEvents), milliseconds. */
 int gst_last_sweep_ms(void* ctx, double* ms);
+
+/* Grams T^T N^-1 [T|r] (gibbs.py:302-304) computed since the last reset, by path (ABI 6):
+ *   counts[0]  persistent kernel, low-rank: the dataset's per-class Grams plus one rank-1
+ *              update per flagged TOA, on the VALU (<= 8 noise classes, <= 32 flagged TOAs,
+ *              every flagged alpha <= 2^20);
+ *   counts[1]  persistent kernel, the n-TOA fp64 MFMA Gram;
+ *   counts[2]  large path, fp64 MFMA Gram (lg_gram / lg_gram_small), chains x launches.
+ * One count per chain per Gram (the floor pass recomputes it: counted again).  Synchronises
+ * the device.  reset != 0 zeroes the counters after reading them. */
+int gst_gram_counts(void* ctx, long long* counts, int reset);
+
+/* Test hook (ABI 6): n draws of the kernel's own samplers into the DEVICE array out, Philox
+ * keyed by (seed, call), for distribution tests of the samplers themselves:
+ *   kind 0  gamma_mt(a): Marsaglia-Tsang Gamma(a, 1), a < 1 by the a + 1 boost (the theta
+ *           stage's Gammas);
+ *   kind 1  Beta(a, b) = Ga / (Ga + Gb) from two gamma_mt draws (update_theta, gibbs.py:196);
+ *   kind 2  gamma_mt_slots<4>, the alpha stage's interleaved Gamma(a) draws (gibbs.py:239);
+ *           n a multiple of 256.
+ * n <= 2^31.  Needs no context; runs on the current device. */
+int gst_debug_variates(int kind, double a, double b, long long n, unsigned long long seed,
+                       unsigned call, double* out, void* stream);
 
 /* Batched synthetic pulsars on the current device: the simulate_data.py:10-39 recipe for
  * `ndatasets` datasets in one launch (one workgroup per dataset), Philox variates keyed by

@@ -157,3 +157,44 @@ def test_low_rank_gram_matches_mfma_gram(name):
     for k in ("b", "alpha", "pout", "theta"):
         r = _rel(a[k][same], b[k][same])
         assert np.all(r <= 1e-8), f"{k}: {r.max():.3e}"
+
+
+@pytest.mark.parametrize("alpha,path", [(30.0, "low_rank"), (1e8, "mfma")])
+def test_low_rank_gram_alpha_gate_and_path_counts(alpha, path):
+    """The low-rank Gram subtracts c_k (1 - 1 / alpha_t) of a class Gram's share per flagged
+    TOA, so a direction fixed by flagged TOAs alone keeps an absolute error ~eps c_k |row|^2
+    against its true size c_k |row|^2 / alpha_t.  The kernel takes it only while
+    every flagged alpha is <= 2^20.  Ten flagged TOAs of J1713 (one noise class): at alpha =
+    30 the Gram runs low-rank, at 1e8 (vvh17's fixed alpha is 1e10) on the MFMA -- counted by
+    gst_gram_counts over a GST_STAGE_GRAM launch -- and the likelihoods at 64 prior draws
+    agree with the forced MFMA Gram to 1e-11 relative (bitwise at 1e8: the same MFMA Gram)."""
+    ref = load_ref("beta_fixed")
+    C, n = 64, ref["pta"].n
+    lo = np.array([p.pmin for p in ref["pta"].params])
+    hi = np.array([p.pmax for p in ref["pta"].params])
+    s0 = sweep_state(ref, 0)
+    z = np.zeros((C, n))
+    z[:, 7:130:13] = 1.0
+    al = np.where(z > 0, alpha, 1.0)
+    st0 = dict(x=np.random.default_rng(4).uniform(lo, hi, size=(C, len(lo))),
+               b=np.tile(s0["b"], (C, 1)), z=z, alpha=al, pout=np.zeros((C, n)),
+               theta=np.full(C, 0.05), nu=np.full(C, 4.0))
+    got, counts = [], []
+    for mfma in (False, True):
+        ns = _native(ref, C, "persistent")
+        ns.set_debug(mfma_gram=mfma)
+        ns.set_state(**st0)
+        got.append(ns.eval_lnlike())
+        ns.gram_counts(reset=True)
+        ns.sweep(1, seed=3, mask=_abi.STAGE_GRAM)
+        counts.append(ns.gram_counts(reset=True))
+        ns.close()
+    assert counts[1] == {"low_rank": 0, "mfma": C, "large_mfma": 0}, counts[1]
+    want = {"low_rank": C, "mfma": 0} if path == "low_rank" else {"low_rank": 0, "mfma": C}
+    assert counts[0] == dict(want, large_mfma=0), counts[0]
+    from test_gpu_parity import _rel
+    np.testing.assert_array_equal(got[0][0], got[1][0])
+    if path == "mfma":
+        np.testing.assert_array_equal(got[0][1], got[1][1])
+    else:
+        assert np.all(_rel(got[0][1], got[1][1]) <= 1e-11), _rel(got[0][1], got[1][1]).max()

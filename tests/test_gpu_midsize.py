@@ -201,3 +201,65 @@ def test_epochs_first_hyper_draws_match_blocked_hyper(dataset):
     for nm, u, v in series:
         p = scipy.stats.ks_2samp(u, v).pvalue
         assert p > 1e-3, f"{nm}: KS p = {p:.2e} (means {u.mean():.4g} / {v.mean():.4g})"
+
+
+def test_overlapping_ecorr_epochs_take_the_general_elimination():
+    """lg_hyper<2> eliminates ECORR epochs first because disjoint epochs make the ECORR block
+    of T^T N^-1 T diagonal.  A basis where TOAs sit in two ECORR columns
+    (nothing enforced it) must run the general elimination instead: the ebig
+    dataset with every 5th TOA also in the next epoch's column, on the large path, gives the
+    b-marginalised likelihood of the oracle (gibbs.py:288-329) at 64 prior draws, within
+    1e-9 relative or the fp64 oracle's own error against the long-double evaluation; the
+    disjoint original keeps the epochs-first kernel, same check."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    import os
+    import warnings
+    from golden_io import GOLDEN
+    from oracle.gibbs_oracle import (ChainState, Oracle, OutlierModel,
+                                     lnlike_marginal_extended)
+    from gibbs_student_t_amd.run_sims import MODELS
+    d = dict(np.load(os.path.join(GOLDEN, "ebig_dataset.npz"), allow_pickle=False))
+    nec = int(d["n_ecorr"])
+    for overlap in (False, True):
+        T = d["T"].copy()
+        m = T.shape[1]
+        if overlap:
+            ec = T[:, m - nec:]
+            for t in range(0, T.shape[0], 5):
+                e = int(np.flatnonzero(ec[t])[0]) if ec[t].any() else 0
+                e2 = (e + 1) % nec
+                if ec[:, e2].any():
+                    T[t, m - nec + e2] = 1.0
+            assert ((T[:, m - nec:] != 0).sum(axis=1) > 1).any()
+        name = str(d["names"][0]).split("_")[0]
+        pta = PTA.from_arrays(name, d["residuals"], d["toaerrs"], T, d["Ffreqs"],
+                              int(d["components"]), float(d["tm_weight"]),
+                              efac=(0.2, 10.0) if int(d["efac_varied"]) else 1.0,
+                              backends=d["backends"], selection=str(d["selection"]),
+                              n_ecorr=nec, ecorr_backend=d["ecorr_backend"],
+                              log10_ecorr=tuple(d["log10_ecorr"]) or None)
+        C2 = 64
+        lo = np.array([p.pmin for p in pta.params])
+        hi = np.array([p.pmax for p in pta.params])
+        x = np.random.default_rng(8).uniform(lo, hi, size=(C2, len(lo)))
+        ns = NativeSampler(pta, MODELS["beta"], 0, path="large")
+        ns.alloc(C2)
+        n = pta.n
+        z = np.zeros((C2, n))
+        z[:, ::17] = 1.0
+        al = np.where(z > 0, 25.0, 1.0)
+        ns.set_state(x=x, z=z, alpha=al, theta=np.full(C2, 0.05), nu=np.full(C2, 4.0))
+        _, h = ns.eval_lnlike()
+        ns.close()
+        orc = Oracle(pta, OutlierModel(**MODELS["beta"]))
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            for k in range(C2):
+                st = ChainState(b=np.zeros(pta.m), z=z[k], alpha=al[k], pout=np.zeros(n),
+                                theta=0.05, nu=4.0)
+                orc.cache = None
+                want64 = orc.lnlike_marginal(st, x[k])
+                ext = lnlike_marginal_extended(pta, st, x[k])
+                tol = max(1e-9 * abs(ext), 4 * abs(want64 - ext))
+                assert abs(h[k] - ext) <= tol, (overlap, k, h[k], ext, want64)
