@@ -24,6 +24,7 @@ DEBUG_LARGE_GRAM = 2
 DEBUG_LARGE_HYPER = 4
 DEBUG_EXACT_BDRAW = 8
 DEBUG_MFMA_GRAM = 16
+DEBUG_EPOCHS_LDS = 32
 STATUS_FLOOR = 16          # status bit 4: a b draw ran at the SVD noise floor
 STATUS_FLAGS = 0xff        # bits 0-7: flags; bits 8..30: the number of floor draws (ABI 5)
 STATUS_ERRORS = STATUS_FLAGS & ~STATUS_FLOOR   # every flag but the informational floor bit

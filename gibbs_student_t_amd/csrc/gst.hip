@@ -756,7 +756,7 @@ static int ensure_scratch(Ctx* cx, int C, hipStream_t st) {
 
 // The red-noise MH block's launches: one per hyper kernel class present (gst_large.hpp
 // hyper_class); a chain of another class returns at once.
-static int launch_hyper(Ctx* cx, gst::LArgs& a, const bool (&hcls)[5], dim3 g8, dim3 b8,
+static int launch_hyper(Ctx* cx, gst::LArgs& a, const bool (&hcls)[7], dim3 g8, dim3 b8,
                         dim3 g16, dim3 b16, dim3 g_chain, dim3 b_chain, hipStream_t st) {
   if (hcls[0]) {
     a.kclass = 8;
@@ -783,6 +783,17 @@ static int launch_hyper(Ctx* cx, gst::LArgs& a, const bool (&hcls)[5], dim3 g8, 
     a.kclass = 2;
     LG_LAUNCH(GST_K_HYPER, gst::lg_hyper<2>, g_chain, b_chain, cx->lds_hyper_ec);
   }
+  // class 2 on one wave per chain (lg_hyper_ecr<MT>, gst_large.hpp ec_reg_mt)
+  if (hcls[5]) {
+    a.kclass = 2;
+    const int w = gst::HE<6>::WPB;
+    LG_LAUNCH(GST_K_HYPER, gst::lg_hyper_ecr<6>, dim3((a.C + w - 1) / w), dim3(64 * w), 0);
+  }
+  if (hcls[6]) {
+    a.kclass = 2;
+    const int w = gst::HE<8>::WPB;
+    LG_LAUNCH(GST_K_HYPER, gst::lg_hyper_ecr<8>, dim3((a.C + w - 1) / w), dim3(64 * w), 0);
+  }
   return 0;
 }
 
@@ -806,12 +817,13 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
   // elimination (lg_hyper_reg<8> / <16>); larger ones: lg_hyper (LDS)
   const int hyper_lds = (cx->debug & GST_DEBUG_LARGE_HYPER) ? 1 : 0;
   bool wcls[3] = {false, false, false}, tcls[2] = {false, false};
-  bool hcls[5] = {false, false, false, false, false};
+  bool hcls[7] = {false, false, false, false, false, false, false};
   for (const gst::DevModel& hm : cx->hmd) {
     wcls[gst::white_class(hm.npad)] = true;
     tcls[gst::toa_class(hm.npad)] = true;
     const int hc = gst::hyper_class_of(hm, hyper_lds);
-    hcls[hc == 8 ? 0 : (hc == 16 ? 1 : (hc == 0 ? 2 : (hc == 1 ? 3 : 4)))] = true;
+    const int emt = gst::ec_reg_mt_of(hm, hyper_lds, cx->debug);
+    hcls[hc == 8 ? 0 : (hc == 16 ? 1 : (hc == 0 ? 2 : (hc == 1 ? 3 : (emt == 6 ? 5 : (emt == 8 ? 6 : 4)))))] = true;
   }
   a.hyper_lds = hyper_lds;
   const dim3 g_hr8((C + gst::HR<8>::WPB - 1) / gst::HR<8>::WPB), b_hr8(64 * gst::HR<8>::WPB);
@@ -1025,7 +1037,7 @@ int gst_set_debug(void* ctx, int flags) {
   Ctx* cx = static_cast<Ctx*>(ctx);
   if (!cx) return fail("gst_set_debug: null ctx");
   if (flags & ~(GST_DEBUG_POISON | GST_DEBUG_LARGE_GRAM | GST_DEBUG_LARGE_HYPER |
-                GST_DEBUG_EXACT_BDRAW | GST_DEBUG_MFMA_GRAM))
+                GST_DEBUG_EXACT_BDRAW | GST_DEBUG_MFMA_GRAM | GST_DEBUG_EPOCHS_LDS))
     return fail("gst_set_debug: unknown flag");
   cx->debug = flags;
   return 0;

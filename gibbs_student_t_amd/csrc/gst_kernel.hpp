@@ -314,6 +314,7 @@ constexpr int STATUS_FLOOR = 16;
 constexpr int STATUS_FLOOR_COUNT = 256;   // one floor draw, counted in bits 8..30
 constexpr int DEBUG_EXACT_BDRAW = 8;
 constexpr int DEBUG_MFMA_GRAM = 16;   // persistent kernel: no low-rank Gram (tests, A/B)
+constexpr int DEBUG_EPOCHS_LDS = 32;  // large path: ECORR-epochs-first chains on lg_hyper<2>
 
 // Smallest / largest pivot over the real columns of a factor whose pivot of internal column
 // j = 64 sl + lane is apr[sl]; real columns are [0, ntm) and [f0, f1) (the rest are unit-prior

@@ -88,6 +88,17 @@ __host__ __device__ constexpr int hyper_class(int hcols, int force_lds, int nec,
 __host__ __device__ inline int hyper_class_of(const DevModel& md, int force_lds) {
   return hyper_class(md.nf + md.nec, force_lds, md.nec, md.ntm + md.nf + 1, md.ec_disjoint);
 }
+// Epochs-first chains (class 2) whose timing model has <= 16 columns and whose Fourier block
+// fits the register layout run lg_hyper_ecr<MT> (one wave per chain, MT = 6 / 8: Fourier
+// blocks of <= 30 / 46 columns) instead of lg_hyper<2>; 0: lg_hyper<2> (also under
+// GST_DEBUG_EPOCHS_LDS or GST_DEBUG_LARGE_HYPER)
+__host__ __device__ constexpr int ec_reg_mt(int hclass, int ntm, int nf, int debug) {
+  return (hclass != 2 || ntm > 16 || (debug & DEBUG_EPOCHS_LDS)) ? 0
+         : (16 + nf <= 8 * 6 - 2 ? 6 : (16 + nf <= 8 * 8 - 2 ? 8 : 0));
+}
+__host__ __device__ inline int ec_reg_mt_of(const DevModel& md, int force_lds, int debug) {
+  return ec_reg_mt(hyper_class_of(md, force_lds), md.ntm, md.nf, debug);
+}
 constexpr int GRAM_WAVES = 8;  // chains per gram workgroup
 #ifndef GST_TM_PW
 #define GST_TM_PW 16   // A/B builds override it (32: config-5 tmelim 1.75 -> 2.95 ms, ebig -20%)
@@ -913,6 +924,7 @@ __global__ void __launch_bounds__(LBLK) lg_hyper(const DevModel* __restrict__ md
   const int c = blockIdx.x;
   const DevModel& md = mds[ds_of(a, c)];
   if (hyper_class_of(md, a.hyper_lds) != MODE) return;   // another class's chain
+  if (EC && ec_reg_mt_of(md, a.hyper_lds, a.st.debug)) return;   // lg_hyper_ecr's chain
   extern __shared__ double lsm[];
   // the hyper-dependent columns: Fourier (power law) then ECORR epochs (10^(2 ecorr_b))
   const int nf = md.nf + md.nec, K0 = md.ntm_pad, mp = md.mp;
@@ -1683,6 +1695,393 @@ __global__ void __launch_bounds__(64 * HR<MT>::WPB) lg_hyper_reg(const DevModel*
       const int k = 64 * cs + lane;
       if (k < i) acc[cs] += aik(i, k) * vi;
     }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// hyper class 2, register-resident (lg_hyper_ecr<MT>): the epochs-first elimination of
+// lg_hyper<2> (ECORR epochs, then the timing model, then the Fourier block) run by ONE wave
+// per chain with the persistent kernel's 8x8-cyclic register elimination, where lg_hyper<2>
+// spends a 256-thread workgroup and ~20 barriers per likelihood on a ~35-row block (round 5:
+// 72% of an ebig sweep).  X's rows in the register layout (X index = internal column):
+//   [TM (ntm) | unit-prior pads to 16 | Fourier (nf) | pads | augmented row at RA | pad]
+// Per distinct ECORR value (a proposal of a log10_ecorr, or the first likelihood):
+//   L = G_xx (+ the timing-model prior) - sum_e g_e g_e^T / a_e,  a_e = G_ee + phi_e^-1,
+// one rank-1 downdate per epoch on the VALU (g_e = G_xe staged through LDS, the lane's rows
+// 8r+p and columns 8s+q read as 128-bit loads), then the timing-model columns eliminated and
+// the whole factor kept in LDS (F); per likelihood the Fourier block's Schur complement is
+// reloaded, phi^-1 added and its columns eliminated (chol_range, paired tail).  log|Sigma| =
+// sum log a_e + log|X's pivots|, d^T Sigma^-1 d likewise.  The b draw back-substitutes X's
+// factor and then each epoch from its pivot and couplings, with lg_hyper<2>'s Philox normals
+// (by internal column): the same elimination order, so the same draws to rounding.
+// ------------------------------------------------------------------------------------
+template <int MT>
+struct HE {
+  static constexpr int RA = 8 * MT - 2;          // augmented row
+  static constexpr int KT = 2;                   // timing-model slot columns (ntm <= 16)
+  static constexpr int WPB = MT <= 6 ? 4 : 2;    // chains (waves) per workgroup
+  static constexpr int KP = kp_for(1);
+  static constexpr int NSL = SL(MT, 0);
+  static constexpr int EG = 8;                   // epochs per staged group
+  // F [NSL][64] the factor (TM slots) + the Fourier block's Schur complement / final factor;
+  // colq, junk, colq2 (chol_range); gq [EG][8][MT] staged coupling rows; ph [64]; mhv
+  // [4 NHYPER]; dx [64] tape Delta by X row; vx [64] the b draw's X solution; the chain's x
+  // and the MH proposal [PMAX] each; the cached ECORR values' phi^-1 [NBMAX]
+  // (wave-uniform values kept in LDS: in registers they cost the 256-register budget of two
+  // chains per SIMD)
+  static constexpr int LDS = 64 * NSL + 8 * MT + 8 * MT + 8 * pair_pw(MT) + EG * 8 * MT + 64 +
+                             4 * NHYPER + 64 + 64 + 2 * PMAX + NBMAX;
+};
+
+template <int MT>
+__global__ void __launch_bounds__(64 * HE<MT>::WPB, 2) lg_hyper_ecr(const DevModel* __restrict__ mds,
+                                                                      LArgs a) {
+  using H = HE<MT>;
+  constexpr int RA = H::RA, NSL = H::NSL, KT = H::KT, WPB = H::WPB, EG = H::EG;
+  static_assert(MT % 2 == 0 && 8 * MT <= 64, "one X row per lane");
+  __shared__ double smem[WPB][H::LDS];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = blockIdx.x * WPB + wv;
+  if (c >= a.C) return;
+  const DevModel& md = mds[ds_of(a, c)];
+  if (ec_reg_mt_of(md, a.hyper_lds, a.st.debug) != MT) return;   // another kernel's chain
+  double* F = smem[wv];
+  double* colq = F + 64 * NSL;
+  double* junk = colq + 8 * MT;
+  double* colq2 = junk + 8 * MT;
+  double* gq = colq2 + 8 * pair_pw(MT);
+  double* ph = gq + EG * 8 * MT;
+  double* mhv = ph + 64;
+  double* dx = mhv + 4 * NHYPER;
+  double* vx = dx + 64;
+  double* xs = vx + 64;        // [PMAX] x
+  double* xqs = xs + PMAX;     // [PMAX] the proposal being evaluated
+  double* phb = xqs + PMAX;    // [NBMAX] phi^-1 (+ f) per backend of the cached elimination
+  const int p = lane >> 3, q = lane & 7;
+  const int nfr = md.nf, nec = md.nec, ntm = md.ntm, K0 = md.ntm_pad, mp = md.mp, P = md.P;
+  double* sc = a.s.sc + (size_t)c * 16;
+  const double fsh = a.floor_pass ? sc[SC_FLOOR] : 0.0;
+  if (a.floor_pass && !(fsh > 0.0)) return;
+  const GDouble* Gg = (const GDouble*)(a.s.G + (size_t)c * mp * mp);   // the raw Gram
+  const Rng rng = make_rng(a, c);
+  const double* tp = tape_row(a, c);
+  if (lane < PMAX) xs[lane] = lane < P ? a.st.x[(size_t)c * P + lane] : 0.0;
+  const double logdetN = sc[SC_LOGDETN], rNr = sc[SC_RNR];
+  const double x_last0 = sc[SC_XLAST];
+  int status = 0;
+  if (!a.eval_only && !a.floor_pass && lane < NHYPER)
+    mh_variate(md, rng, tp, NWHITE + lane, mhv + 4 * lane);
+  // internal column of X row i (-1: a unit-prior pad); X rows are internal columns (K0 = 16)
+  auto gxi = [&](int i) __attribute__((always_inline)) {
+    return (i < ntm || (i >= 16 && i < 16 + nfr)) ? i : (i == RA ? md.raug : -1);
+  };
+  const int gl = gxi(lane);   // this lane's X row (epoch downdates, b draw)
+  // per-lane copies of what every likelihood reads (a global load inside the MH loop is a full
+  // memory latency per likelihood, and the scalar ones share lgkmcnt with the LDS traffic):
+  // lane 16 + f: log f, log df of Fourier column f; lane b < nb: backend b's ecorr index and
+  // epoch count, and the ECORR value of the cached elimination
+  const int fl_ = lane - 16;
+  const double lf_l = (fl_ >= 0 && fl_ < nfr) ? md.lfreq[fl_] : 0.0;
+  const double ldf_l = (fl_ >= 0 && fl_ < nfr) ? md.ldf[fl_] : 0.0;
+  const int pib = lane < md.nb ? md.ecorr_b[lane] : -1;
+  const double ecc = lane < md.nb ? md.ec_count[lane] : 0.0;
+  const int iA = md.idx_logA, iG = md.idx_gamma, nb = md.nb, raug = md.raug;
+  double eck_l = 0.0;
+  double L[NSL];
+  // cache of the last ECORR values' elimination (wave-uniform) and the TM columns' harvest
+  bool ecvalid = false;
+  double lde = 0.0, qde = 0.0, aemin = INFINITY, aemax = 0.0, tm_ld = 0.0, tm_quad = 0.0;
+  int fle = 0, tm_fail = 0;
+  double tm_apr = 1.0, tm_zr = 0.0, f_apr = 1.0, f_zr = 0.0;   // lane k: column k's pivot, aug
+  auto phe = [&](int e) __attribute__((always_inline)) { return phb[md.ecb[e]]; };
+  lds_order();
+
+  // the b-marginalised lnL (gibbs.py:288-329) at the proposal in xqs
+  auto lnl = [&](int& failed) __attribute__((always_inline)) -> double {
+    const double lA = xqs[iA];
+    const double g = xqs[iG];
+    const double lc = 2.0 * lA * 2.302585092994045684 - md.log_12pi2 + (g - 3.0) * md.log_fyr;
+    ph[lane] = (fl_ >= 0 && fl_ < nfr) ? exp(-(lc - g * lf_l + ldf_l)) + fsh : 0.0;
+    double logdet_phi = ((double)nfr * lc - g * md.sum_lfreq + md.sum_ldf) + md.logdet_phi_tm;
+    const double xb = pib >= 0 ? xqs[pib] : 0.0;   // lane b: backend b's log10_ecorr
+    const double tb_ = ecc > 0.0 ? ecc * (2.0 * xb * 2.302585092994045684) : 0.0;
+#pragma unroll
+    for (int b = 0; b < NBMAX; ++b)   // backend by backend, as lg_hyper<2>
+      if (b < nb) logdet_phi += rdlane(tb_, b);
+    const bool same = ecvalid && __ballot(pib >= 0 && xb != eck_l) == 0ull;
+    CholCtx cc{colq, junk, colq2, lane, p, q, RA, 1.0, 0.0, 0, 0, {1.0, 1.0}, {0.0, 0.0}};
+    if (!same) {
+      if (lane < NBMAX) phb[lane] = pib >= 0 ? exp(-2.0 * xb * 2.302585092994045684) + fsh : 0.0;
+      eck_l = xb;
+      // L = G_xx at the lane's slots (+ the timing-model prior; unit pads)
+#pragma unroll
+      for (int r = 0; r < MT; ++r)
+#pragma unroll
+        for (int s2 = 0; s2 <= r; ++s2) {
+          int i = 8 * r + p, j = 8 * s2 + q;
+          if (j > i) { const int t = i; i = j; j = t; }
+          const int gi = gxi(i), gj = gxi(j);
+          double v = (i == j) ? 1.0 : 0.0;
+          if (gi >= 0 && gj >= 0) v = Gg[(size_t)gi * mp + gj];
+          if (i == j && i < ntm) v = (v + md.tm_phiinv) + fsh;
+          L[SL(r, s2)] = v;
+        }
+      lds_order();
+      // the epochs, 64 per block, EG per group: L -= g_e g_e^T / a_e with g_e = G_xe staged in
+      // LDS as [p][r] (the lane's rows 8r+p and columns 8s+q contiguous, 128-bit loads); the
+      // block's 1 / a_e computed lane-parallel up front and read by readlane (no scalar memory
+      // op in the loop: those share lgkmcnt with the LDS staging and would expose their
+      // latency every group); the next group's coupling loads issued before this group's
+      // downdates
+      const int rr = lane >> 3, pp = lane & 7;   // this lane's X row 8 rr + pp
+      const int e_end = K0 + nfr + nec;
+      auto gload = [&](int ge) __attribute__((always_inline)) -> double {
+        if (ge >= e_end || gl < 0) return 0.0;
+        return gl == raug ? Gg[(size_t)raug * mp + ge] : Gg[(size_t)ge * mp + gl];
+      };
+#pragma unroll 1
+      for (int eb = 0; eb < nec; eb += 64) {
+        const int ne = nec - eb < 64 ? nec - eb : 64;
+        double yeb = 0.0;   // lane u: 1 / a_e of epoch eb + u
+        if (lane < ne) {
+          const int ge = K0 + nfr + eb + lane;
+          yeb = 1.0 / (Gg[(size_t)ge * mp + ge] + phe(eb + lane));
+        }
+        double gn[EG];
+#pragma unroll
+        for (int u = 0; u < EG; ++u) gn[u] = gload(K0 + nfr + eb + u);
+#pragma unroll 1
+        for (int u0 = 0; u0 < ne; u0 += EG) {
+          double gcur[EG];
+#pragma unroll
+          for (int u = 0; u < EG; ++u) gcur[u] = gn[u];
+          const int gnext = K0 + nfr + eb + u0 + EG;
+#pragma unroll
+          for (int u = 0; u < EG; ++u) gn[u] = (u0 + EG + u < ne) ? gload(gnext + u) : 0.0;
+          lds_order();   // the previous group's reads precede these stores
+#pragma unroll
+          for (int u = 0; u < EG; ++u)
+            if (rr < MT) gq[u * 8 * MT + pp * MT + rr] = gcur[u];
+          lds_order();
+#pragma unroll
+          for (int u = 0; u < EG; ++u) {
+            if (u0 + u >= ne) break;
+            typedef double v2_t __attribute__((ext_vector_type(2)));
+            double gr[MT], gc[MT];
+            const double* bp = gq + u * 8 * MT + p * MT;
+            const double* bq = gq + u * 8 * MT + q * MT;
+#pragma unroll
+            for (int r = 0; r < MT; r += 2) {
+              const v2_t x0 = *(const v2_t*)(bp + r), x1 = *(const v2_t*)(bq + r);
+              gr[r] = x0[0];
+              gr[r + 1] = x0[1];
+              gc[r] = x1[0];
+              gc[r + 1] = x1[1];
+            }
+            const double ye = rdlane(yeb, u0 + u);
+#pragma unroll
+            for (int r = 0; r < MT; ++r) {
+              const double t = gr[r] * ye;
+#pragma unroll
+              for (int s2 = 0; s2 <= r; ++s2) L[SL(r, s2)] = fma(-t, gc[s2], L[SL(r, s2)]);
+            }
+          }
+        }
+      }
+      // the epochs' pivots and augmented-row terms (lane-parallel over epochs)
+      double l_ = 0.0, q_ = 0.0, mn = INFINITY, mx = 0.0;
+      int f_ = 0;
+      for (int e = lane; e < nec; e += 64) {
+        const int ge = K0 + nfr + e;
+        const double ae = Gg[(size_t)ge * mp + ge] + phe(e);
+        const double zr = Gg[(size_t)raug * mp + ge];
+        f_ |= !(ae > 0.0) ? 1 : 0;
+        l_ += log(ae);
+        q_ += zr * zr * (1.0 / ae);
+        mn = fmin(mn, ae);
+        mx = fmax(mx, ae);
+      }
+      lde = wave_sum(l_);
+      qde = wave_sum(q_);
+      fle = __ballot(f_) != 0ull ? 1 : 0;
+      aemin = -wave_max(-mn);
+      aemax = wave_max(mx);
+      // the timing-model columns, kept with the epochs' elimination
+      chol_range<MT, 0, 16, H::KP>(L, cc);
+      chol_harvest<MT, 0, 16, RA>(L, cc);
+      chol_stats<0, 16>(cc);
+      tm_ld = log(cc.mant) + (double)cc.expo * 0.693147180559945309417;
+      tm_quad = cc.quad;
+      tm_fail = cc.fail;
+      tm_apr = cc.apr[0];
+      tm_zr = cc.zr[0];
+#pragma unroll
+      for (int sl = 0; sl < NSL; ++sl) F[64 * sl + lane] = L[sl];
+      ecvalid = true;
+      cc = CholCtx{colq, junk, colq2, lane, p, q, RA, 1.0, 0.0, 0, 0, {1.0, 1.0}, {0.0, 0.0}};
+    } else {
+#pragma unroll
+      for (int r = KT; r < MT; ++r)
+#pragma unroll
+        for (int s2 = KT; s2 <= r; ++s2) L[SL(r, s2)] = F[64 * SL(r, s2) + lane];
+    }
+    lds_order();
+    // + the Fourier priors on the diagonal, then the Fourier block's columns
+#pragma unroll
+    for (int r = KT; r < MT; ++r)
+      if (p == q) L[SL(r, r)] += ph[8 * r + p];
+    chol_range<MT, KT, RA, H::KP>(L, cc);
+    chol_harvest<MT, 16, RA, RA>(L, cc);
+    chol_stats<16, RA>(cc);
+    f_apr = cc.apr[0];
+    f_zr = cc.zr[0];
+    failed = (cc.fail | tm_fail | fle) != 0;
+    if (failed) return -INFINITY;
+    const double ld = log(cc.mant) + (double)cc.expo * 0.693147180559945309417;
+    double ll = -0.5 * (logdetN + rNr);
+    ll += 0.5 * ((tm_quad + qde + cc.quad) - (tm_ld + lde + ld) - logdet_phi);
+    return ll;
+  };
+  // the proposal in xqs within the prior box (lnprior, gibbs.py:337-339)
+  auto in_prior = [&]() __attribute__((always_inline)) {
+    const bool out = lane < P && !(xqs[lane] >= md.pmin[lane] && xqs[lane] <= md.pmax[lane]);
+    return __ballot(out) == 0ull;
+  };
+
+  const bool run = (a.mask & 6u) || a.eval_only;
+  bool redraw = false, Lvalid = false;
+  int fb = 0;
+  if (run) {
+    double l0 = 0.0, p0 = 0.0;
+    // the floor pass refactors the final x only (its MH decisions stand)
+    const int first = ((a.mask & 2u) || a.eval_only) && !a.floor_pass ? -1 : NHYPER;
+    for (int step = first; step <= NHYPER; ++step) {
+      double luacc = 0.0;
+      if (step == NHYPER) {
+        if (a.eval_only || !(a.mask & 4u)) break;
+        // gibbs.py:373: every element of x differs from the sweep's starting last parameter
+        redraw = __ballot(lane < P && xs[lane] == x_last0) == 0ull;
+        if (a.mask & 128u) redraw = true;
+        if (!redraw || Lvalid) break;
+      }
+      lds_order();
+      if (step < 0 || step == NHYPER) {
+        if (lane < PMAX) xqs[lane] = xs[lane];
+      } else {
+        const int par = (int)mhv[4 * step + 0];
+        const double delta = mhv[4 * step + 1];
+        if (lane < PMAX) xqs[lane] = (lane == par) ? xs[lane] + delta : xs[lane];
+        luacc = mhv[4 * step + 2];
+      }
+      lds_order();
+      const double p1 = in_prior() ? md.lp_sum : -INFINITY;
+      if (step >= 0 && step < NHYPER && p1 == -INFINITY) continue;
+      int f1 = 0;
+      const double l1 = lnl(f1);
+      if (step == NHYPER) {
+        fb = f1;
+        break;
+      }
+      if (f1) status |= 1;
+      if (step < 0) {
+        l0 = l1;
+        p0 = p1;
+        Lvalid = !f1;   // see lg_hyper
+        if (a.eval_only) {
+          if (lane == 0) a.out_h[c] = l1;
+          break;
+        }
+        continue;
+      }
+      if ((l1 + p1) - (l0 + p0) > luacc) {
+        if (lane < PMAX) xs[lane] = xqs[lane];
+        l0 = l1;
+        p0 = p1;
+        Lvalid = true;
+      } else {
+        Lvalid = false;
+      }
+    }
+  }
+  if (a.eval_only) return;
+  lds_order();
+  // the SVD noise floor (floor_shift): the epochs' pivots, then X's real columns (timing
+  // model, Fourier), as lg_hyper<2>
+  double fs = 0.0;
+  const double apx = lane < 16 ? tm_apr : f_apr;   // pivot of X column `lane`
+  const double zrx = lane < 16 ? tm_zr : f_zr;
+  if (!a.floor_pass && redraw && !fb && !(a.st.debug & DEBUG_EXACT_BDRAW)) {
+    double mn, mx;
+    const double ap[2] = {apx, 1.0};
+    pivot_range(ap, lane, ntm, 16, 16 + nfr, mn, mx);
+    fs = floor_of(fmin(mn, aemin), fmax(mx, aemax));
+  }
+  if (lane < P) a.st.x[(size_t)c * P + lane] = xs[lane];
+  if (lane == 0) {
+    sc[SC_REDRAW] = redraw ? 1.0 : 0.0;
+    sc[SC_FB] = (double)fb;
+    if (!a.floor_pass) sc[SC_FLOOR] = fs;
+    if (a.st.status)
+      a.st.status[c] = (a.st.status[c] | status | ((redraw && fb) ? 2 : 0) |
+                        (fs > 0.0 ? STATUS_FLOOR : 0)) +
+                       ((fs > 0.0 && !a.floor_pass) ? STATUS_FLOOR_COUNT : 0);
+  }
+  if (!redraw || fb || fs > 0.0) return;   // fs > 0: the floor pass draws b
+  // b draw: X's factor -- the timing-model slots in F since the last ECORR elimination (the
+  // ECORR values of x), the Fourier block's from the registers -- then the epochs.  Reference
+  // order [Fourier | TM | ECORR]: X row i < ntm is b[nf + i], row 16 + f is b[f].
+#pragma unroll
+  for (int r = KT; r < MT; ++r)
+#pragma unroll
+    for (int s2 = KT; s2 <= r; ++s2) F[64 * SL(r, s2) + lane] = L[SL(r, s2)];
+  const int refx = lane < ntm ? nfr + lane : ((lane >= 16 && lane < 16 + nfr) ? lane - 16 : -1);
+  if (tp) dx[lane] = refx >= 0 ? tp[TP_DELTA + refx] : 0.0;
+  lds_order();
+  auto aik = [&](int i, int k) __attribute__((always_inline)) {
+    return F[64 * SL(i >> 3, k >> 3) + 8 * (i & 7) + (k & 7)];
+  };
+  const bool real = refx >= 0;
+  const double yk = real ? rsqrt_nr(apx) : 0.0;
+  double w = 0.0;
+  if (real) {
+    if (tp) {
+      // eta_k = y_k sum_{i >= k} a_ik Delta_i (so that L^-T eta = Delta)
+      double s = 0.0;
+      for (int i = lane; i < RA; ++i) s += aik(i, lane) * dx[i];
+      w = (zrx + s) * yk;
+    } else {
+      w = zrx * yk + normal_k(rng, (uint32_t)lane, TAG_BDRAW);   // X row = internal column
+    }
+  }
+  double acc = 0.0;   // acc_k = sum_{i > k} a_ik v_i
+  double* brow = a.st.b + (size_t)c * md.m;
+  for (int i = RA - 1; i >= 0; --i) {
+    const double yi = rdlane(yk, i), wi = rdlane(w, i), ai = rdlane(acc, i);
+    const double vi = (wi - yi * ai) * yi;
+    if (lane == 0) vx[i] = vi;
+    if (lane < i) acc += aik(i, lane) * vi;
+  }
+  lds_order();
+  if (refx >= 0) brow[refx] = vx[lane];
+  // the epochs: v_e = (w_e - y_e sum_x G_xe v_x) y_e, w_e = z_e y_e + eta_e
+  for (int e = lane; e < nec; e += 64) {
+    const int ge = K0 + nfr + e;
+    const double ae = Gg[(size_t)ge * mp + ge] + phe(e), ye = rsqrt_nr(ae);
+    double sx = 0.0;
+    for (int i = 0; i < 16 + nfr; ++i)
+      if (i < ntm || i >= 16) sx += Gg[(size_t)ge * mp + i] * vx[i];
+    const double zr = Gg[(size_t)md.raug * mp + ge];
+    double we;
+    if (tp) {
+      double s = ae * tp[TP_DELTA + nfr + ntm + e];
+      for (int i = 0; i < 16 + nfr; ++i)
+        if (i < ntm || i >= 16) s += Gg[(size_t)ge * mp + i] * dx[i];
+      we = (zr + s) * ye;
+    } else {
+      we = zr * ye + normal_k(rng, (uint32_t)ge, TAG_BDRAW);
+    }
+    brow[nfr + ntm + e] = (we - ye * sx) * ye;
   }
 }
 

@@ -158,18 +158,20 @@ class NativeSampler:
 
     def set_debug(self, poison: bool = False, large_gram: bool = False,
                   large_hyper: bool = False, exact_bdraw: bool = False,
-                  mfma_gram: bool = False):
+                  mfma_gram: bool = False, epochs_lds: bool = False):
         """gst_set_debug: GST_DEBUG_POISON overwrites every chain's LDS and parked scratch
         with NaN at each sweep start (a check that no sweep reads stale state);
         GST_DEBUG_LARGE_GRAM / _HYPER force the large path's generic Gram / hyper kernels
         (tests compare them with the mid-size kernels); GST_DEBUG_EXACT_BDRAW draws b from
         Sigma exactly also beyond fp64 resolution (no SVD noise floor, include/gst.h);
         GST_DEBUG_MFMA_GRAM keeps the persistent kernel's Gram on the MFMA path (no low-rank
-        Gram)."""
+        Gram); GST_DEBUG_EPOCHS_LDS runs ECORR-epochs-first chains on the 256-thread lg_hyper<2>
+        instead of the one-wave lg_hyper_ecr."""
         flags = ((_abi.DEBUG_POISON if poison else 0) | (_abi.DEBUG_LARGE_GRAM if large_gram else 0)
                  | (_abi.DEBUG_LARGE_HYPER if large_hyper else 0)
                  | (_abi.DEBUG_EXACT_BDRAW if exact_bdraw else 0)
-                 | (_abi.DEBUG_MFMA_GRAM if mfma_gram else 0))
+                 | (_abi.DEBUG_MFMA_GRAM if mfma_gram else 0)
+                 | (_abi.DEBUG_EPOCHS_LDS if epochs_lds else 0))
         _abi.check(self.lib, self.lib.gst_set_debug(self.ctx, flags), "gst_set_debug")
 
     # ---- state ---------------------------------------------------------------------

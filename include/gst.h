@@ -264,12 +264,17 @@ int gst_set_waves(void* ctx, int waves);
  * never the low-rank one (datasets of <= 8 noise classes, at most 32 flagged TOAs: the
  * per-class Grams plus one rank-1 update per flagged TOA); the two agree
  * to rounding. */
+/* GST_DEBUG_EPOCHS_LDS (ABI 6): large-path chains whose ECORR epochs are eliminated first run
+ * the 256-thread LDS kernel lg_hyper<2> instead of the one-wave register kernel
+ * lg_hyper_ecr (timing model <= 16 columns, Fourier block <= 46 columns); same elimination
+ * order, likelihoods and b draws equal to rounding.  A/B and test switch. */
 enum gst_debug {
   GST_DEBUG_POISON = 1,
   GST_DEBUG_LARGE_GRAM = 2,
   GST_DEBUG_LARGE_HYPER = 4,
   GST_DEBUG_EXACT_BDRAW = 8,
-  GST_DEBUG_MFMA_GRAM = 16
+  GST_DEBUG_MFMA_GRAM = 16,
+  GST_DEBUG_EPOCHS_LDS = 32
 };
 int gst_set_debug(void* ctx, int flags);
 

@@ -263,3 +263,66 @@ def test_overlapping_ecorr_epochs_take_the_general_elimination():
                 ext = lnlike_marginal_extended(pta, st, x[k])
                 tol = max(1e-9 * abs(ext), 4 * abs(want64 - ext))
                 assert abs(h[k] - ext) <= tol, (overlap, k, h[k], ext, want64)
+
+
+@pytest.mark.parametrize("name", ["ebig_beta_fixed", "ebig_t_fixed", "mb_beta_fixed",
+                                  "mb_t_fixed", "mbn_vvh17_fixed"])
+def test_register_epochs_first_matches_lds_epochs_first(name):
+    """lg_hyper_ecr (round 6: the epochs-first elimination on one wave per chain, register-
+    resident 8x8-cyclic factor, the epochs' rank-1 downdates on the VALU) against lg_hyper<2>
+    (256 threads, LDS, MFMA rank update; GST_DEBUG_EPOCHS_LDS): the same elimination order
+    [ECORR | TM | Fourier] and Philox normals, so the b-marginalised likelihood agrees to
+    1e-10 at 256 states (prior draws, the fixture's latents) and 16 chains x 6 sweeps from
+    the fixture's start make the same MH, z and nu decisions with b, alpha, pout, theta within
+    1e-8 relative."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    from golden_io import load_ref, sweep_state
+    ref = load_ref(name)
+    pta = ref["pta"]
+    s0 = sweep_state(ref, 0)
+    C2 = 256
+    lo = np.array([p.pmin for p in pta.params])
+    hi = np.array([p.pmax for p in pta.params])
+    x = np.random.default_rng(12).uniform(lo, hi, size=(C2, len(lo)))
+    got, outs = [], []
+    for lds in (False, True):
+        ns = NativeSampler(pta, ref["kw"], 0, path="large")
+        ns.set_debug(epochs_lds=lds)
+        ns.alloc(C2)
+        ns.set_state(x=x, b=np.tile(s0["b"], (C2, 1)), z=np.tile(s0["z"], (C2, 1)),
+                     alpha=np.tile(s0["alpha"], (C2, 1)), pout=np.tile(s0["pout"], (C2, 1)),
+                     theta=np.full(C2, s0["theta"]), nu=np.full(C2, s0["nu"]))
+        got.append(ns.eval_lnlike())
+        ns.close()
+        ns = NativeSampler(pta, ref["kw"], 0, path="large")
+        ns.set_debug(epochs_lds=lds)
+        ns.alloc(C)
+        ns.set_state(x=np.tile(ref["xs"], (C, 1)), b=np.tile(s0["b"], (C, 1)),
+                     z=np.tile(s0["z"], (C, 1)), alpha=np.tile(s0["alpha"], (C, 1)),
+                     pout=np.tile(s0["pout"], (C, 1)), theta=np.full(C, s0["theta"]),
+                     nu=np.full(C, s0["nu"]))
+        rec = ns.alloc_records(S)
+        ns.sweep(S, records=rec, seed=35)
+        out = {k: v.cpu().numpy() for k, v in rec.items()}
+        out["status"] = ns.get_state()["status"]
+        ns.close()
+        outs.append(out)
+    (w1, h1), (w2, h2) = got
+    np.testing.assert_array_equal(w1, w2)
+    ok = np.isfinite(h2)
+    assert ok.sum() > C2 // 2
+    np.testing.assert_array_equal(np.isfinite(h1), ok)
+    r = np.abs(h1[ok] - h2[ok]) / np.abs(h2[ok])
+    assert r.max() <= 1e-10, r.max()
+    a, b = outs
+    assert np.all((a["status"] & STATUS_ERRORS) == 0)
+    np.testing.assert_array_equal(a["status"], b["status"])
+    for k in ("x", "z", "nu"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    eb = np.linalg.norm(a["b"] - b["b"], axis=-1) / np.maximum(np.linalg.norm(b["b"], axis=-1),
+                                                                1e-300)
+    assert np.all(eb <= 1e-8), ("b", eb.max())
+    for k in ("alpha", "pout", "theta"):
+        d = np.abs(a[k] - b[k])
+        assert np.all(d <= 1e-8 * np.maximum(np.abs(b[k]), 1e-300) + 1e-300), (k, d.max())
