@@ -1848,17 +1848,25 @@ __global__ void __launch_bounds__(64 * HE<MT>::WPB, 2) lg_hyper_ecr(const DevMod
           const int ge = K0 + nfr + eb + lane;
           yeb = 1.0 / (Gg[(size_t)ge * mp + ge] + phe(eb + lane));
         }
-        double gn[EG];
+        // two groups of loads in flight (a coupling row comes from HBM / MALL: one group of
+        // downdates does not cover its latency)
+        double gn[EG], gn2[EG];
 #pragma unroll
-        for (int u = 0; u < EG; ++u) gn[u] = gload(K0 + nfr + eb + u);
+        for (int u = 0; u < EG; ++u) {
+          gn[u] = gload(K0 + nfr + eb + u);
+          gn2[u] = (EG + u < ne) ? gload(K0 + nfr + eb + EG + u) : 0.0;
+        }
 #pragma unroll 1
         for (int u0 = 0; u0 < ne; u0 += EG) {
           double gcur[EG];
 #pragma unroll
-          for (int u = 0; u < EG; ++u) gcur[u] = gn[u];
-          const int gnext = K0 + nfr + eb + u0 + EG;
+          for (int u = 0; u < EG; ++u) {
+            gcur[u] = gn[u];
+            gn[u] = gn2[u];
+          }
+          const int gnext = K0 + nfr + eb + u0 + 2 * EG;
 #pragma unroll
-          for (int u = 0; u < EG; ++u) gn[u] = (u0 + EG + u < ne) ? gload(gnext + u) : 0.0;
+          for (int u = 0; u < EG; ++u) gn2[u] = (u0 + 2 * EG + u < ne) ? gload(gnext + u) : 0.0;
           lds_order();   // the previous group's reads precede these stores
 #pragma unroll
           for (int u = 0; u < EG; ++u)
