@@ -323,6 +323,10 @@ def test_register_epochs_first_matches_lds_epochs_first(name):
     eb = np.linalg.norm(a["b"] - b["b"], axis=-1) / np.maximum(np.linalg.norm(b["b"], axis=-1),
                                                                 1e-300)
     assert np.all(eb <= 1e-8), ("b", eb.max())
+    # (pout is a probability: within 1e-8 relative or 1e-9 absolute -- vvh17's Sigma reaches
+    # cond ~ 1e22, where the two eliminations' b draws differ by cond x eps in the directions
+    # the data leave free, which moves the small pout values of the flagged TOAs at 1e-10)
     for k in ("alpha", "pout", "theta"):
         d = np.abs(a[k] - b[k])
-        assert np.all(d <= 1e-8 * np.maximum(np.abs(b[k]), 1e-300) + 1e-300), (k, d.max())
+        tol = 1e-8 * np.maximum(np.abs(b[k]), 1e-300) + (1e-9 if k == "pout" else 1e-300)
+        assert np.all(d <= tol), (k, d.max())
