@@ -783,16 +783,18 @@ static int launch_hyper(Ctx* cx, gst::LArgs& a, const bool (&hcls)[7], dim3 g8, 
     a.kclass = 2;
     LG_LAUNCH(GST_K_HYPER, gst::lg_hyper<2>, g_chain, b_chain, cx->lds_hyper_ec);
   }
-  // class 2 on one wave per chain (lg_hyper_ecr<MT>, gst_large.hpp ec_reg_mt)
+  // class 2 on one wave per chain (lg_hyper_ecr<MT, RA>, gst_large.hpp ec_reg_mt)
   if (hcls[5]) {
     a.kclass = 2;
-    const int w = gst::HE<6>::WPB;
-    LG_LAUNCH(GST_K_HYPER, gst::lg_hyper_ecr<6>, dim3((a.C + w - 1) / w), dim3(64 * w), 0);
+    const int w = gst::HE<6, 46>::WPB;
+    const auto kern = &gst::lg_hyper_ecr<6, 46>;
+    LG_LAUNCH(GST_K_HYPER, kern, dim3((a.C + w - 1) / w), dim3(64 * w), 0);
   }
   if (hcls[6]) {
     a.kclass = 2;
-    const int w = gst::HE<8>::WPB;
-    LG_LAUNCH(GST_K_HYPER, gst::lg_hyper_ecr<8>, dim3((a.C + w - 1) / w), dim3(64 * w), 0);
+    const int w = gst::HE<8, 62>::WPB;
+    const auto kern = &gst::lg_hyper_ecr<8, 62>;
+    LG_LAUNCH(GST_K_HYPER, kern, dim3((a.C + w - 1) / w), dim3(64 * w), 0);
   }
   return 0;
 }
@@ -823,7 +825,7 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
     tcls[gst::toa_class(hm.npad)] = true;
     const int hc = gst::hyper_class_of(hm, hyper_lds);
     const int emt = gst::ec_reg_mt_of(hm, hyper_lds, cx->debug);
-    hcls[hc == 8 ? 0 : (hc == 16 ? 1 : (hc == 0 ? 2 : (hc == 1 ? 3 : (emt == 6 ? 5 : (emt == 8 ? 6 : 4)))))] = true;
+    hcls[hc == 8 ? 0 : (hc == 16 ? 1 : (hc == 0 ? 2 : (hc == 1 ? 3 : (emt > 0 ? 4 + emt : 4))))] = true;
   }
   a.hyper_lds = hyper_lds;
   const dim3 g_hr8((C + gst::HR<8>::WPB - 1) / gst::HR<8>::WPB), b_hr8(64 * gst::HR<8>::WPB);

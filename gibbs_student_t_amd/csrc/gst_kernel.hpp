@@ -67,7 +67,10 @@ constexpr int LR_MAX = 32;
 constexpr double LR_ALPHA_MAX = 0x1p20;   // ... and alpha_t <= 2^20 on every flagged TOA
 // the largest TOA-slot count whose two-chains-per-SIMD build the host picks (wider shapes
 // run one chain per SIMD)
-constexpr int OCC2_NS_MAX = 8;
+#ifndef GST_OCC2_NS_MAX
+#define GST_OCC2_NS_MAX 8   // A/B builds override it (GST_EXTRA_CFLAGS=-DGST_OCC2_NS_MAX=16)
+#endif
+constexpr int OCC2_NS_MAX = GST_OCC2_NS_MAX;
 __host__ __device__ constexpr int pair_pw(int MT) { return MT - KP_MIN; }
 #ifndef GST_KP_OCC2
 #define GST_KP_OCC2 6   // A/B builds override it (GST_EXTRA_CFLAGS=-DGST_KP_OCC2=...)

@@ -89,15 +89,20 @@ __host__ __device__ inline int hyper_class_of(const DevModel& md, int force_lds)
   return hyper_class(md.nf + md.nec, force_lds, md.nec, md.ntm + md.nf + 1, md.ec_disjoint);
 }
 // Epochs-first chains (class 2) whose timing model has <= 16 columns and whose Fourier block
-// fits the register layout run lg_hyper_ecr<MT> (one wave per chain, MT = 6 / 8: Fourier
+// fits the register layout run lg_hyper_ecr<MT, RA> (one wave per chain, MT = 6 / 8: Fourier
 // blocks of <= 30 / 46 columns) instead of lg_hyper<2>; 0: lg_hyper<2> (also under
 // GST_DEBUG_EPOCHS_LDS or GST_DEBUG_LARGE_HYPER)
-__host__ __device__ constexpr int ec_reg_mt(int hclass, int ntm, int nf, int debug) {
-  return (hclass != 2 || ntm > 16 || (debug & DEBUG_EPOCHS_LDS)) ? 0
-         : (16 + nf <= 8 * 6 - 2 ? 6 : (16 + nf <= 8 * 8 - 2 ? 8 : 0));
+// (instance id: 1 = <6, 46>, 2 = <8, 62>: (MT, augmented row); an instance <6, 38> for
+// Fourier blocks of <= 22 columns, cutting eight pad steps, spilled 148 B/lane and measured
+// no faster on ebig / mb)
+// (and at most EC_REG_MAX epochs: their pivots and augmented-row entries live in registers)
+constexpr int EC_REG_MAX = 192;
+__host__ __device__ constexpr int ec_reg_mt(int hclass, int ntm, int nf, int nec, int debug) {
+  return (hclass != 2 || ntm > 16 || nec > EC_REG_MAX || (debug & DEBUG_EPOCHS_LDS)) ? 0
+         : (16 + nf <= 46 ? 1 : (16 + nf <= 62 ? 2 : 0));
 }
 __host__ __device__ inline int ec_reg_mt_of(const DevModel& md, int force_lds, int debug) {
-  return ec_reg_mt(hyper_class_of(md, force_lds), md.ntm, md.nf, debug);
+  return ec_reg_mt(hyper_class_of(md, force_lds), md.ntm, md.nf, md.nec, debug);
 }
 constexpr int GRAM_WAVES = 8;  // chains per gram workgroup
 #ifndef GST_TM_PW
@@ -1699,7 +1704,7 @@ __global__ void __launch_bounds__(64 * HR<MT>::WPB) lg_hyper_reg(const DevModel*
 }
 
 // ------------------------------------------------------------------------------------
-// hyper class 2, register-resident (lg_hyper_ecr<MT>): the epochs-first elimination of
+// hyper class 2, register-resident (lg_hyper_ecr<MT, RA>): the epochs-first elimination of
 // lg_hyper<2> (ECORR epochs, then the timing model, then the Fourier block) run by ONE wave
 // per chain with the persistent kernel's 8x8-cyclic register elimination, where lg_hyper<2>
 // spends a 256-thread workgroup and ~20 barriers per likelihood on a ~35-row block (round 5:
@@ -1714,38 +1719,47 @@ __global__ void __launch_bounds__(64 * HR<MT>::WPB) lg_hyper_reg(const DevModel*
 // sum log a_e + log|X's pivots|, d^T Sigma^-1 d likewise.  The b draw back-substitutes X's
 // factor and then each epoch from its pivot and couplings, with lg_hyper<2>'s Philox normals
 // (by internal column): the same elimination order, so the same draws to rounding.
+// The kernel is latency-bound, not issue-bound: everything it reads more than once from the
+// Gram is fetched once into LDS (each epoch's G_ee, its augmented-row entry and backend:
+// nec <= EC_REG_MAX), the coupling rows stream two groups ahead, and the per-lane model data
+// every likelihood reads are copied into registers once.
 // ------------------------------------------------------------------------------------
-template <int MT>
+constexpr int EC_NEB = 3;                   // 64-epoch blocks (EC_REG_MAX = 64 EC_NEB)
+template <int MT, int RA_>
 struct HE {
-  static constexpr int RA = 8 * MT - 2;          // augmented row
+  static constexpr int RA = RA_;                 // augmented row (<= 8 MT - 2)
+  static constexpr int ID = MT == 8 ? 2 : 1;     // ec_reg_mt's instance id
   static constexpr int KT = 2;                   // timing-model slot columns (ntm <= 16)
-  static constexpr int WPB = MT <= 6 ? 4 : 2;    // chains (waves) per workgroup
+  static constexpr int WPB = MT <= 6 ? 4 : 2;    // chains (waves) per workgroup (he_wpb)
   static constexpr int KP = kp_for(1);
   static constexpr int NSL = SL(MT, 0);
-  static constexpr int EG = 8;                   // epochs per staged group
+  static constexpr int EG = 4;                   // epochs per staged group
   // F [NSL][64] the factor (TM slots) + the Fourier block's Schur complement / final factor;
   // colq, junk, colq2 (chol_range); gq [EG][8][MT] staged coupling rows; ph [64]; mhv
   // [4 NHYPER]; dx [64] tape Delta by X row; vx [64] the b draw's X solution; the chain's x
-  // and the MH proposal [PMAX] each; the cached ECORR values' phi^-1 [NBMAX]
-  // (wave-uniform values kept in LDS: in registers they cost the 256-register budget of two
-  // chains per SIMD)
+  // and the MH proposal [PMAX] each; the cached ECORR values' phi^-1 [NBMAX]; each epoch's
+  // G_ee, augmented-row entry and backend [EC_REG_MAX] each (wave-uniform and per-epoch
+  // values kept in LDS: in registers they cost the 256-register budget of two chains per
+  // SIMD; 20 KB per chain, two 4-chain workgroups per CU)
   static constexpr int LDS = 64 * NSL + 8 * MT + 8 * MT + 8 * pair_pw(MT) + EG * 8 * MT + 64 +
-                             4 * NHYPER + 64 + 64 + 2 * PMAX + NBMAX;
+                             4 * NHYPER + 64 + 64 + 2 * PMAX + NBMAX + 3 * 64 * EC_NEB;
 };
 
-template <int MT>
-__global__ void __launch_bounds__(64 * HE<MT>::WPB, 2) lg_hyper_ecr(const DevModel* __restrict__ mds,
+__host__ __device__ constexpr int he_wpb(int MT) { return MT <= 6 ? 4 : 2; }
+template <int MT, int RA_>
+__global__ void __launch_bounds__(64 * he_wpb(MT), 2) lg_hyper_ecr(const DevModel* __restrict__ mds,
                                                                       LArgs a) {
-  using H = HE<MT>;
+  using H = HE<MT, RA_>;
   constexpr int RA = H::RA, NSL = H::NSL, KT = H::KT, WPB = H::WPB, EG = H::EG;
-  static_assert(MT % 2 == 0 && 8 * MT <= 64, "one X row per lane");
+  static_assert(MT % 2 == 0 && 8 * MT <= 64 && RA % 2 == 0 && RA <= 8 * MT - 2,
+                "one X row per lane");
   __shared__ double smem[WPB][H::LDS];
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = blockIdx.x * WPB + wv;
   if (c >= a.C) return;
   const DevModel& md = mds[ds_of(a, c)];
-  if (ec_reg_mt_of(md, a.hyper_lds, a.st.debug) != MT) return;   // another kernel's chain
+  if (ec_reg_mt_of(md, a.hyper_lds, a.st.debug) != H::ID) return;   // another kernel's chain
   double* F = smem[wv];
   double* colq = F + 64 * NSL;
   double* junk = colq + 8 * MT;
@@ -1758,6 +1772,9 @@ __global__ void __launch_bounds__(64 * HE<MT>::WPB, 2) lg_hyper_ecr(const DevMod
   double* xs = vx + 64;        // [PMAX] x
   double* xqs = xs + PMAX;     // [PMAX] the proposal being evaluated
   double* phb = xqs + PMAX;    // [NBMAX] phi^-1 (+ f) per backend of the cached elimination
+  double* ege = phb + NBMAX;   // [EC_REG_MAX] G_ee of epoch e
+  double* ezr = ege + 64 * EC_NEB;   // [EC_REG_MAX] z_e = G_{r,e}
+  double* ebd = ezr + 64 * EC_NEB;   // [EC_REG_MAX] the epoch's backend
   const int p = lane >> 3, q = lane & 7;
   const int nfr = md.nf, nec = md.nec, ntm = md.ntm, K0 = md.ntm_pad, mp = md.mp, P = md.P;
   double* sc = a.s.sc + (size_t)c * 16;
@@ -1777,6 +1794,7 @@ __global__ void __launch_bounds__(64 * HE<MT>::WPB, 2) lg_hyper_ecr(const DevMod
     return (i < ntm || (i >= 16 && i < 16 + nfr)) ? i : (i == RA ? md.raug : -1);
   };
   const int gl = gxi(lane);   // this lane's X row (epoch downdates, b draw)
+  const int raug = md.raug, nb = md.nb;
   // per-lane copies of what every likelihood reads (a global load inside the MH loop is a full
   // memory latency per likelihood, and the scalar ones share lgkmcnt with the LDS traffic):
   // lane 16 + f: log f, log df of Fourier column f; lane b < nb: backend b's ecorr index and
@@ -1784,17 +1802,25 @@ __global__ void __launch_bounds__(64 * HE<MT>::WPB, 2) lg_hyper_ecr(const DevMod
   const int fl_ = lane - 16;
   const double lf_l = (fl_ >= 0 && fl_ < nfr) ? md.lfreq[fl_] : 0.0;
   const double ldf_l = (fl_ >= 0 && fl_ < nfr) ? md.ldf[fl_] : 0.0;
-  const int pib = lane < md.nb ? md.ecorr_b[lane] : -1;
-  const double ecc = lane < md.nb ? md.ec_count[lane] : 0.0;
-  const int iA = md.idx_logA, iG = md.idx_gamma, nb = md.nb, raug = md.raug;
-  double eck_l = 0.0;
+  const int pib = lane < nb ? md.ecorr_b[lane] : -1;
+  const double ecc = lane < nb ? md.ec_count[lane] : 0.0;
+  const int iA = md.idx_logA, iG = md.idx_gamma;
+  // epochs e: G_ee, the augmented-row entry z_e = G_{r,e} and the backend
+#pragma unroll
+  for (int k = 0; k < EC_NEB; ++k) {
+    const int e = 64 * k + lane, ge = K0 + nfr + e;
+    const bool v = e < nec;
+    ege[e] = v ? Gg[(size_t)ge * mp + ge] : 1.0;
+    ezr[e] = v ? Gg[(size_t)raug * mp + ge] : 0.0;
+    ebd[e] = v ? (double)md.ecb[e] : 0.0;
+  }
   double L[NSL];
   // cache of the last ECORR values' elimination (wave-uniform) and the TM columns' harvest
   bool ecvalid = false;
   double lde = 0.0, qde = 0.0, aemin = INFINITY, aemax = 0.0, tm_ld = 0.0, tm_quad = 0.0;
   int fle = 0, tm_fail = 0;
   double tm_apr = 1.0, tm_zr = 0.0, f_apr = 1.0, f_zr = 0.0;   // lane k: column k's pivot, aug
-  auto phe = [&](int e) __attribute__((always_inline)) { return phb[md.ecb[e]]; };
+  double eck_l = 0.0;
   lds_order();
 
   // the b-marginalised lnL (gibbs.py:288-329) at the proposal in xqs
@@ -1814,48 +1840,55 @@ __global__ void __launch_bounds__(64 * HE<MT>::WPB, 2) lg_hyper_ecr(const DevMod
     if (!same) {
       if (lane < NBMAX) phb[lane] = pib >= 0 ? exp(-2.0 * xb * 2.302585092994045684) + fsh : 0.0;
       eck_l = xb;
-      // L = G_xx at the lane's slots (+ the timing-model prior; unit pads)
-#pragma unroll
-      for (int r = 0; r < MT; ++r)
-#pragma unroll
-        for (int s2 = 0; s2 <= r; ++s2) {
-          int i = 8 * r + p, j = 8 * s2 + q;
-          if (j > i) { const int t = i; i = j; j = t; }
-          const int gi = gxi(i), gj = gxi(j);
-          double v = (i == j) ? 1.0 : 0.0;
-          if (gi >= 0 && gj >= 0) v = Gg[(size_t)gi * mp + gj];
-          if (i == j && i < ntm) v = (v + md.tm_phiinv) + fsh;
-          L[SL(r, s2)] = v;
-        }
-      lds_order();
-      // the epochs, 64 per block, EG per group: L -= g_e g_e^T / a_e with g_e = G_xe staged in
-      // LDS as [p][r] (the lane's rows 8r+p and columns 8s+q contiguous, 128-bit loads); the
-      // block's 1 / a_e computed lane-parallel up front and read by readlane (no scalar memory
-      // op in the loop: those share lgkmcnt with the LDS staging and would expose their
-      // latency every group); the next group's coupling loads issued before this group's
-      // downdates
+      // the epochs' coupling rows g_e (lane = X row), two groups of EG in flight
       const int rr = lane >> 3, pp = lane & 7;   // this lane's X row 8 rr + pp
       const int e_end = K0 + nfr + nec;
       auto gload = [&](int ge) __attribute__((always_inline)) -> double {
         if (ge >= e_end || gl < 0) return 0.0;
         return gl == raug ? Gg[(size_t)raug * mp + ge] : Gg[(size_t)ge * mp + gl];
       };
-#pragma unroll 1
-      for (int eb = 0; eb < nec; eb += 64) {
-        const int ne = nec - eb < 64 ? nec - eb : 64;
-        double yeb = 0.0;   // lane u: 1 / a_e of epoch eb + u
-        if (lane < ne) {
-          const int ge = K0 + nfr + eb + lane;
-          yeb = 1.0 / (Gg[(size_t)ge * mp + ge] + phe(eb + lane));
-        }
-        // two groups of loads in flight (a coupling row comes from HBM / MALL: one group of
-        // downdates does not cover its latency)
-        double gn[EG], gn2[EG];
+      double gn[EG], gn2[EG];
 #pragma unroll
-        for (int u = 0; u < EG; ++u) {
-          gn[u] = gload(K0 + nfr + eb + u);
-          gn2[u] = (EG + u < ne) ? gload(K0 + nfr + eb + EG + u) : 0.0;
+      for (int u = 0; u < EG; ++u) {
+        gn[u] = gload(K0 + nfr + u);
+        gn2[u] = gload(K0 + nfr + EG + u);
+      }
+      lds_order();
+      // a_e = G_ee + phi^-1 of its backend, 1 / a_e, and the epochs' likelihood terms
+      double yek[EC_NEB];
+      {
+        double l_ = 0.0, q_ = 0.0, mn = INFINITY, mx = 0.0;
+        int f_ = 0;
+#pragma unroll
+        for (int k = 0; k < EC_NEB; ++k) {
+          const int e = 64 * k + lane;
+          const bool v = e < nec;
+          const double ae = ege[e] + phb[(int)ebd[e]];
+          yek[k] = v ? 1.0 / ae : 0.0;
+          if (v) {
+            const double zr = ezr[e];
+            f_ |= !(ae > 0.0) ? 1 : 0;
+            l_ += log(ae);
+            q_ += zr * zr * (1.0 / ae);
+            mn = fmin(mn, ae);
+            mx = fmax(mx, ae);
+          }
         }
+        lde = wave_sum(l_);
+        qde = wave_sum(q_);
+        fle = __ballot(f_) != 0ull ? 1 : 0;
+        aemin = -wave_max(-mn);
+        aemax = wave_max(mx);
+      }
+      // L = -sum_e g_e g_e^T / a_e: 64 epochs per block (1 / a_e by readlane), EG per group,
+      // g_e staged in LDS as [p][r] (the lane's rows 8r+p and columns 8s+q contiguous)
+#pragma unroll
+      for (int sl = 0; sl < NSL; ++sl) L[sl] = 0.0;
+#pragma unroll
+      for (int k = 0; k < EC_NEB; ++k) {
+        const int eb = 64 * k;
+        if (eb >= nec) break;
+        const int ne = nec - eb < 64 ? nec - eb : 64;
 #pragma unroll 1
         for (int u0 = 0; u0 < ne; u0 += EG) {
           double gcur[EG];
@@ -1864,9 +1897,9 @@ __global__ void __launch_bounds__(64 * HE<MT>::WPB, 2) lg_hyper_ecr(const DevMod
             gcur[u] = gn[u];
             gn[u] = gn2[u];
           }
-          const int gnext = K0 + nfr + eb + u0 + 2 * EG;
+          const int gnext = K0 + nfr + eb + u0 + 2 * EG;   // (rows past this block: the next)
 #pragma unroll
-          for (int u = 0; u < EG; ++u) gn2[u] = (u0 + 2 * EG + u < ne) ? gload(gnext + u) : 0.0;
+          for (int u = 0; u < EG; ++u) gn2[u] = gload(gnext + u);
           lds_order();   // the previous group's reads precede these stores
 #pragma unroll
           for (int u = 0; u < EG; ++u)
@@ -1887,7 +1920,7 @@ __global__ void __launch_bounds__(64 * HE<MT>::WPB, 2) lg_hyper_ecr(const DevMod
               gc[r] = x1[0];
               gc[r + 1] = x1[1];
             }
-            const double ye = rdlane(yeb, u0 + u);
+            const double ye = rdlane(yek[k], u0 + u);
 #pragma unroll
             for (int r = 0; r < MT; ++r) {
               const double t = gr[r] * ye;
@@ -1897,24 +1930,18 @@ __global__ void __launch_bounds__(64 * HE<MT>::WPB, 2) lg_hyper_ecr(const DevMod
           }
         }
       }
-      // the epochs' pivots and augmented-row terms (lane-parallel over epochs)
-      double l_ = 0.0, q_ = 0.0, mn = INFINITY, mx = 0.0;
-      int f_ = 0;
-      for (int e = lane; e < nec; e += 64) {
-        const int ge = K0 + nfr + e;
-        const double ae = Gg[(size_t)ge * mp + ge] + phe(e);
-        const double zr = Gg[(size_t)raug * mp + ge];
-        f_ |= !(ae > 0.0) ? 1 : 0;
-        l_ += log(ae);
-        q_ += zr * zr * (1.0 / ae);
-        mn = fmin(mn, ae);
-        mx = fmax(mx, ae);
-      }
-      lde = wave_sum(l_);
-      qde = wave_sum(q_);
-      fle = __ballot(f_) != 0ull ? 1 : 0;
-      aemin = -wave_max(-mn);
-      aemax = wave_max(mx);
+      // + G_xx at the lane's slots and the timing-model prior (unit pads)
+#pragma unroll
+      for (int r = 0; r < MT; ++r)
+#pragma unroll
+        for (int s2 = 0; s2 <= r; ++s2) {
+          int i = 8 * r + p, j = 8 * s2 + q;
+          if (j > i) { const int t = i; i = j; j = t; }
+          const int gi = gxi(i), gj = gxi(j);
+          double v = (gi >= 0 && gj >= 0) ? Gg[(size_t)gi * mp + gj] : (i == j ? 1.0 : 0.0);
+          if (i == j && i < ntm) v = (v + md.tm_phiinv) + fsh;
+          L[SL(r, s2)] = v + L[SL(r, s2)];
+        }
       // the timing-model columns, kept with the epochs' elimination
       chol_range<MT, 0, 16, H::KP>(L, cc);
       chol_harvest<MT, 0, 16, RA>(L, cc);
@@ -1952,8 +1979,9 @@ __global__ void __launch_bounds__(64 * HE<MT>::WPB, 2) lg_hyper_ecr(const DevMod
     return ll;
   };
   // the proposal in xqs within the prior box (lnprior, gibbs.py:337-339)
+  const double pmin_l = lane < P ? md.pmin[lane] : 0.0, pmax_l = lane < P ? md.pmax[lane] : 0.0;
   auto in_prior = [&]() __attribute__((always_inline)) {
-    const bool out = lane < P && !(xqs[lane] >= md.pmin[lane] && xqs[lane] <= md.pmax[lane]);
+    const bool out = lane < P && !(xqs[lane] >= pmin_l && xqs[lane] <= pmax_l);
     return __ballot(out) == 0ull;
   };
 
@@ -2072,19 +2100,36 @@ __global__ void __launch_bounds__(64 * HE<MT>::WPB, 2) lg_hyper_ecr(const DevMod
   }
   lds_order();
   if (refx >= 0) brow[refx] = vx[lane];
-  // the epochs: v_e = (w_e - y_e sum_x G_xe v_x) y_e, w_e = z_e y_e + eta_e
-  for (int e = lane; e < nec; e += 64) {
+  // the epochs: v_e = (w_e - y_e sum_x G_xe v_x) y_e, w_e = z_e y_e + eta_e.  A lane's epoch
+  // row G_e,[0, RA) is read with every load issued before the first use (a loop of dependent
+  // load -> FMA steps cost a memory latency per X row); pad rows carry v = 0 (and zero or
+  // another epoch's exact-zero coupling), so the sum over all RA rows in row order is the sum
+  // over the real ones
+#pragma unroll
+  for (int k = 0; k < EC_NEB; ++k) {
+    const int e = 64 * k + lane;
+    if (e >= nec) continue;
     const int ge = K0 + nfr + e;
-    const double ae = Gg[(size_t)ge * mp + ge] + phe(e), ye = rsqrt_nr(ae);
+    const double ae = ege[e] + phb[(int)ebd[e]], ye = rsqrt_nr(ae);
+    const double zr = ezr[e];
+    typedef double v2_t __attribute__((ext_vector_type(2)));
+    const __attribute__((address_space(1))) v2_t* grow =
+        (const __attribute__((address_space(1))) v2_t*)(Gg + (size_t)ge * mp);
+    double gx_[RA];
+#pragma unroll
+    for (int i = 0; i < RA; i += 2) {
+      const v2_t v = grow[i / 2];
+      gx_[i] = v[0];
+      gx_[i + 1] = v[1];
+    }
     double sx = 0.0;
-    for (int i = 0; i < 16 + nfr; ++i)
-      if (i < ntm || i >= 16) sx += Gg[(size_t)ge * mp + i] * vx[i];
-    const double zr = Gg[(size_t)md.raug * mp + ge];
+#pragma unroll
+    for (int i = 0; i < RA; ++i) sx += gx_[i] * vx[i];
     double we;
     if (tp) {
       double s = ae * tp[TP_DELTA + nfr + ntm + e];
-      for (int i = 0; i < 16 + nfr; ++i)
-        if (i < ntm || i >= 16) s += Gg[(size_t)ge * mp + i] * dx[i];
+#pragma unroll
+      for (int i = 0; i < RA; ++i) s += gx_[i] * dx[i];
       we = (zr + s) * ye;
     } else {
       we = zr * ye + normal_k(rng, (uint32_t)ge, TAG_BDRAW);
