@@ -2,7 +2,8 @@
 persistent kernel's GEN instances against the large path, same dataset and start.
 
     python tools/gen_rate.py [sweeps] [datasets]     e.g. python tools/gen_rate.py 200 ecb,ecq
-    (GR_PATHS=large: the large path only, e.g. for ebig's 150-column red-noise / ECORR block)
+    (GR_PATHS=large: the large path only, e.g. for ebig's 150-column red-noise / ECORR block;
+     GR_DEBUG=epochs_lds[,...]: NativeSampler.set_debug flags)
 
 Datasets are the golden ones (tests/golden/<name>_dataset.npz); the model is bench.py's
 (outlier mixture, beta theta prior, varied nu), chains start from prior draws.
@@ -25,6 +26,8 @@ from gibbs_student_t_amd.native import NativeSampler  # noqa: E402
 
 def rate(pta, path, C, S, W=20):
     ns = NativeSampler(pta, CFG, 0, path=path)
+    if os.environ.get("GR_DEBUG"):      # e.g. GR_DEBUG=epochs_lds (A/B of a kernel choice)
+        ns.set_debug(**{k: True for k in os.environ["GR_DEBUG"].split(",")})
     ns.alloc(C)
     ns.set_state(**initial_state(pta, C, 0))
     ns.sweep(W, seed=3)
