@@ -210,6 +210,33 @@ __device__ __forceinline__ void block_sum3(double& a, double& b, double& c, doub
   c = (red3[8] + red3[9]) + (red3[10] + red3[11]);
 }
 
+// K deterministic block sums behind one pair of barriers, each bitwise block_sum<NW>'s;
+// red: [K][NW]
+template <int NW, int K>
+__device__ __forceinline__ void block_sum_k(double (&v)[K], double* red) {
+#pragma unroll
+  for (int j = 0; j < K; ++j) v[j] = wave_sum(v[j]);
+  if constexpr (NW == 1) {
+    (void)red;
+    return;
+  }
+  const int wv = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) red[j * NW + wv] = v[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const double* r = red + j * NW;
+    double sum = 0.0;
+#pragma unroll
+    for (int h = 0; h < NW; h += 4) sum += (r[h] + r[h + 1]) + (r[h + 2] + r[h + 3]);
+    v[j] = sum;
+  }
+}
+
 // MH variates of global step gs (0..19 white, 20..29 hyper) exactly as the persistent
 // kernel draws them (gst_kernel.hpp mh_variates): parameter, jump, log(u_acc), 10^(2 jump).
 __device__ __forceinline__ void mh_variate(const DevModel& md, const Rng& rng, const double* tp,
@@ -265,10 +292,15 @@ __device__ __forceinline__ double lnpriorP(const DevModel& md, const XVec& xq) {
 }
 
 // x[i] for a wave-uniform or per-thread runtime index (a select chain: no scratch array)
+// (the empty asm keeps r in a register between the selects: without it the compiler turns the
+// chain back into an indexed load, which puts the whole of x in scratch memory)
 __device__ __forceinline__ double xget(const XVec& x, int i) {
   double r = x[0];
 #pragma unroll
-  for (int j = 1; j < PMAX; ++j) r = (i == j) ? x[j] : r;
+  for (int j = 1; j < PMAX; ++j) {
+    r = (i == j) ? x[j] : r;
+    asm volatile("" : "+v"(r));
+  }
   return r;
 }
 
@@ -314,7 +346,11 @@ __device__ __forceinline__ WhiteNoise white_noise(const DevModel& md, const XVec
 #pragma unroll
   for (int b = 0; b < NBMAX; ++b) {
     if (b < md.nb) {
-      const double ef = md.efac_b[b] >= 0 ? xget(x, md.efac_b[b]) : md.efac_const;
+      // (value selects, not a pointer select between x and md: that made the compiler load
+      // through a flat pointer into the private x array)
+      const int ei = md.efac_b[b];
+      const double xe = xget(x, ei >= 0 ? ei : 0);
+      const double ef = ei >= 0 ? xe : md.efac_const;
       w.ef2[b] = ef * ef;
       w.Q[b] = exp(2.0 * xget(x, md.equad_b[b]) * 2.302585092994045684);
     } else {
@@ -362,6 +398,8 @@ __global__ void __launch_bounds__(TB) lg_white(const DevModel* __restrict__ mds,
     a.st.status[c] |= 4;                          // bad dataset index (ran on dataset 0)
   if (white_class(md.npad) != a.kclass) return;   // another class's launch runs this chain
   __shared__ double red[TB / 64];
+  __shared__ double redk[7 * (TB / 64)];   // lnlk: [2 K + 1][waves]
+  __shared__ double wtab[3][2][NBMAX];     // the pass's candidates: efac_b^2, Q_b
   __shared__ double mhv[NWHITE][4];
   constexpr int WU = TB == 64 ? 8 : 4;   // TOAs per thread per round of the per-TOA loops
   const int n = md.n, nst = a.st.nst, npad = md.npad;
@@ -378,95 +416,216 @@ __global__ void __launch_bounds__(TB) lg_white(const DevModel* __restrict__ mds,
   const bool do_white = (a.mask & 1u) || a.eval_only;
 
   if (do_white) {
-    // fixed over the block: a_t = alpha_t^z_t, y_t^2 / a_t and sum log a_t
-    // (U TOAs per thread per round, their loads issued first: one load round trip per round,
-    // not per TOA; the TOAs past n in the last round are masked)
-    double la = 0.0;
-    for (int t0 = threadIdx.x; t0 < n; t0 += WU * TB) {
-      double zv[WU], av[WU], yw[WU];
-#pragma unroll
-      for (int k = 0; k < WU; ++k) {
-        const int t = t0 + k * TB < n ? t0 + k * TB : min((int)threadIdx.x, n - 1);  // in-bounds, masked below
-        zv[k] = zc[t];
-        av[k] = alc[t];
-        yw[k] = yc[t];
-      }
-#pragma unroll
-      for (int k = 0; k < WU; ++k) {
-        if (t0 + k * TB >= n) continue;
-        const bool zt = zv[k] != 0.0;
-        const double at = zt ? av[k] : 1.0;
-        if (zt) la += log(at);
-        wc[t0 + k * TB] = yw[k] * yw[k] / at;
-      }
-    }
-    la = block_sum<TB / 64>(la, red);
     if (!a.eval_only && threadIdx.x < NWHITE) mh_variate(md, rng, tp, threadIdx.x, mhv[threadIdx.x]);
     __syncthreads();
     // a proposal's variances come from its parameters, except that Q of a one-backend model
     // moves by 10^(2 delta) with its equad (the MH variate's 4th entry), as the persistent
-    // kernel carries it
-    auto lnl = [&](const WhiteNoise& wn) -> double {
-      double sq = 0.0;
-      LogProd lp;
-      // one backend: four TOAs' loads in flight per round (the passes were latency-bound at
-      // one load and one full wait per TOA); t order kept, so the sums are unchanged
-      if (wn.nb <= 1) {
-        const double e = wn.ef2[0], q = wn.Q[0];
-        const GDouble* s2 = (const GDouble*)wn.s2;
-        const GDouble* w2 = (const GDouble*)wc;
-        // WU TOAs per thread per round, all loads issued first; the last round's TOAs past
-        // n are masked (they read TOA threadIdx.x and contribute factor 1 / term 0)
-        constexpr int U = WU;
-        for (int t0 = threadIdx.x; t0 < n; t0 += U * TB) {
-          double sv[U], wv[U];
+    // kernel carries it.
+    // K likelihoods per pass over the TOAs (the pass streams the chain's y^2 / a row from
+    // HBM, 800 KB at 100k TOAs; K = 3 costs VALU work, not bytes).  The block's first pass
+    // (FIRST) reads z, alpha and y instead and leaves y_t^2 / a_t (a_t = alpha_t^z_t) in the
+    // w row for the later passes, with sum log a_t.  Per TOA and likelihood: N0 (one FMA),
+    // its reciprocal (estimate + one Newton step, ~2e-15 relative) times y^2 / a into the sum,
+    // and N0 into a product of U factors (N0 ~ 1e-22 .. 1e-6 s^2: no under/overflow in 4)
+    // that enters the mantissa / exponent accumulation once per round.
+    double la = 0.0;
+    auto lnlk = [&](auto kc, auto first_c, auto& out) __attribute__((always_inline)) {
+      constexpr int K = decltype(kc)::value;
+      constexpr bool FIRST = decltype(first_c)::value;
+      double sq[K], lsv[2 * K + 1];
+      LogProd lp[K];
+      double lat = 0.0;   // FIRST: this thread's sum log a_t
 #pragma unroll
-          for (int k = 0; k < U; ++k) {
-            const int t = t0 + k * TB < n ? t0 + k * TB : min((int)threadIdx.x, n - 1);  // in-bounds, masked below
-            sv[k] = s2[t];
-            wv[k] = w2[t];
-          }
+      for (int j = 0; j < K; ++j) sq[j] = 0.0;
+      // one backend: WU TOAs' loads in flight per round (the passes were latency-bound at one
+      // load and one full wait per TOA)
+      if (md.nb <= 1) {
+        double e[K], q[K];
 #pragma unroll
-          for (int k = 0; k < U; ++k) {
-            const bool in = t0 + k * TB < n;
-            const double N0 = e * sv[k] + q;
-            lp.mul(in ? N0 : 1.0);
-            sq += in ? div_pos(wv[k], N0) : 0.0;
-          }
+        for (int j = 0; j < K; ++j) {
+          e[j] = wtab[j][0][0];
+          q[j] = wtab[j][1][0];
         }
+        const GDouble* s2 = (const GDouble*)md.sig2;
+        const GDouble* w2 = (const GDouble*)wc;
+        // WU TOAs per thread per round, all loads issued first (the first pass's four loads
+        // per TOA: four TOAs per round); full rounds run unmasked, the last partial round is
+        // masked (its TOAs past n read TOA threadIdx.x and contribute factor 1 / term 0)
+        constexpr int U = FIRST ? 4 : WU;
+        auto round = [&](int t0, auto masked_c) __attribute__((always_inline)) {
+          constexpr bool M = decltype(masked_c)::value;
+          double sv[U], wv[U], zv[U], av[U];
+#pragma unroll
+          for (int k = 0; k < U; ++k) {
+            const int t = !M || t0 + k * TB < n ? t0 + k * TB : min((int)threadIdx.x, n - 1);
+            sv[k] = s2[t];
+            if constexpr (FIRST) {
+              zv[k] = zc[t];
+              av[k] = alc[t];
+              wv[k] = yc[t];
+            } else {
+              wv[k] = w2[t];
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < U; ++k) {
+            const bool in = !M || t0 + k * TB < n;
+            if constexpr (FIRST) {
+              // w_t = y_t^2 / a_t, a_t = alpha_t^z_t; log 1 = 0 exactly, so only outliers add
+              // to sum log a_t
+              const bool zt = in && zv[k] != 0.0;
+              const double at = zt ? av[k] : 1.0;
+              lat += log(at);
+              const double w = wv[k] * wv[k] / at;
+              if (in) wc[t0 + k * TB] = w;
+              wv[k] = w;
+            }
+            if constexpr (M) wv[k] = in ? wv[k] : 0.0;
+          }
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            double pr = 1.0;
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+              double N0 = e[j] * sv[k] + q[j];
+              if constexpr (M) N0 = t0 + k * TB < n ? N0 : 1.0;
+              pr *= N0;
+              sq[j] = fma(wv[k], rcp_nr1(N0), sq[j]);
+            }
+            lp[j].mul(pr);
+          }
+        };
+        int t0 = threadIdx.x;
+        for (; t0 + (U - 1) * TB < n; t0 += U * TB) round(t0, std::false_type{});
+        if (t0 < n) round(t0, std::true_type{});
       } else {
         for (int t = threadIdx.x; t < n; t += TB) {
-          const double N0 = wn.n0(t);
-          lp.mul(N0);
-          sq += div_pos(wc[t], N0);
+          const double sv = md.sig2[t];
+          const int b = md.bk[t];
+          double wt;
+          if constexpr (FIRST) {
+            const double at = zc[t] != 0.0 ? alc[t] : 1.0;
+            const double yt = yc[t];
+            lat += log(at);
+            wt = yt * yt / at;
+            wc[t] = wt;
+          } else {
+            wt = wc[t];
+          }
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            const double N0 = wtab[j][0][b] * sv + wtab[j][1][b];
+            lp[j].mul(N0);
+            sq[j] = fma(wt, rcp_nr1(N0), sq[j]);
+          }
         }
       }
-      const double sl = block_sum<TB / 64>(lp.log_sum(), red);
-      sq = block_sum<TB / 64>(sq, red);
-      return -0.5 * ((la + sl) + sq);
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        lsv[2 * j] = lp[j].log_sum();
+        lsv[2 * j + 1] = sq[j];
+      }
+      lsv[2 * K] = lat;
+      block_sum_k<TB / 64, 2 * K + 1>(lsv, redk);
+      if constexpr (FIRST) la = lsv[2 * K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) out[j] = -0.5 * ((la + lsv[2 * j]) + lsv[2 * j + 1]);
     };
-    WhiteNoise wx = white_noise(md, xv);
-    double l0 = lnl(wx), p0 = lnpriorP(md, xv);
+    // The candidates' variances wait in LDS (wtab[j]: efac_b^2 and Q_b of every backend, one
+    // thread per backend), so that only the chain's own x lives in registers across a pass
+    // (three proposals' parameter vectors and variance sets held there cost ~190 registers
+    // and spilled).  A proposal is (x0, Q0) moved by its step's jump; Q of a one-backend
+    // model is carried multiplicatively (Q0 10^(2 delta) when the step moves equad).
+    constexpr double LN10 = 2.302585092994045684;
+    auto propose = [&](int step, const XVec& x0, double Q0, XVec& qv, double& Qq)
+        __attribute__((always_inline)) {
+      const int par = (int)mhv[step][0];
+#pragma unroll
+      for (int j = 0; j < PMAX; ++j) qv[j] = (j == par) ? x0[j] + mhv[step][1] : x0[j];
+      Qq = (par == md.idx_equad) ? Q0 * mhv[step][3] : Q0;
+    };
+    auto stage = [&](int j, const XVec& qv, double Qq) __attribute__((always_inline)) {
+      const int b = threadIdx.x;
+      if (b < md.nb) {
+        const int ei = md.efac_b[b];
+        const double xe = xget(qv, ei >= 0 ? ei : 0);
+        const double ef = ei >= 0 ? xe : md.efac_const;
+        wtab[j][0][b] = ef * ef;
+        wtab[j][1][b] = md.nb <= 1 ? Qq : exp(2.0 * xget(qv, md.equad_b[b]) * LN10);
+      }
+    };
+    double Qx = exp(2.0 * xget(xv, md.equad_b[0]) * LN10);   // (one backend: the carried Q)
+    double l0, p0 = lnpriorP(md, xv);
+    stage(0, xv, Qx);
     if (a.eval_only) {
+      __syncthreads();
+      double l1v[1];
+      lnlk(std::integral_constant<int, 1>{}, std::true_type{}, l1v);
+      l0 = l1v[0];
       if (threadIdx.x == 0) a.out_w[c] = l0;
     } else {
-      for (int step = 0; step < NWHITE; ++step) {
-        const int par = (int)mhv[step][0];
-        XVec q;
+      // MH steps two per pass (gibbs.py:114-143 runs them one at a time): a pass evaluates
+      // step s's proposal from the current state and both possible proposals of step s + 1
+      // (from the state step s rejects to, and from the one it accepts to), so the 21
+      // likelihoods of the block take 11 passes over the TOAs.  Decisions, proposals and
+      // values are exactly the sequential loop's (a proposal outside the prior is evaluated
+      // and ignored, where the loop skips it); proposals are recomputed, not kept, after a
+      // pass.
+      auto settle = [&](int step, const XVec& x0, double Q0, double l1)
+          __attribute__((always_inline)) -> bool {
+        XVec qv;
+        double Qq;
+        propose(step, x0, Q0, qv, Qq);
+        const double p1 = lnpriorP(md, qv);
+        const bool acc = p1 != -INFINITY && (l1 + p1) - (l0 + p0) > mhv[step][2];
+        if (acc) {
 #pragma unroll
-        for (int j = 0; j < PMAX; ++j) q[j] = (j == par) ? xv[j] + mhv[step][1] : xv[j];
-        WhiteNoise wq = white_noise(md, q);
-        if (md.nb <= 1) wq.Q[0] = (par == md.idx_equad) ? wx.Q[0] * mhv[step][3] : wx.Q[0];
-        const double p1 = lnpriorP(md, q);
-        if (p1 == -INFINITY) continue;
-        const double l1 = lnl(wq);
-        if ((l1 + p1) - (l0 + p0) > mhv[step][2]) {
-#pragma unroll
-          for (int j = 0; j < PMAX; ++j) xv[j] = q[j];
+          for (int j = 0; j < PMAX; ++j) xv[j] = qv[j];
           l0 = l1;
           p0 = p1;
-          wx = wq;
+          Qx = Qq;
         }
+        return acc;
+      };
+      {  // pass 0: the current state and step 0's proposal
+        {
+          XVec q0;
+          double Q0;
+          propose(0, xv, Qx, q0, Q0);
+          stage(1, q0, Q0);
+        }
+        __syncthreads();
+        double lv[2];
+        lnlk(std::integral_constant<int, 2>{}, std::true_type{}, lv);
+        l0 = lv[0];
+        settle(0, xv, Qx, lv[1]);
+      }
+      for (int step = 1; step < NWHITE; step += 2) {
+        const bool two = step + 1 < NWHITE;
+        {
+          XVec qs, qo;
+          double Qs, Qo;
+          propose(step, xv, Qx, qs, Qs);
+          stage(0, qs, Qs);
+          if (two) {
+            propose(step + 1, xv, Qx, qo, Qo);     // step s rejected
+            stage(1, qo, Qo);
+            propose(step + 1, qs, Qs, qo, Qo);     // step s accepted
+            stage(2, qo, Qo);
+          }
+        }
+        __syncthreads();
+        double lv[3];
+        if (two) {
+          lnlk(std::integral_constant<int, 3>{}, std::false_type{}, lv);
+        } else {
+          double l1v[1];
+          lnlk(std::integral_constant<int, 1>{}, std::false_type{}, l1v);
+          lv[0] = l1v[0];
+        }
+        const bool acc = settle(step, xv, Qx, lv[0]);
+        // step s + 1 from the state step s left (xv, Qx are already that state)
+        if (two) settle(step + 1, xv, Qx, acc ? lv[2] : lv[1]);
       }
       if (threadIdx.x < md.P) a.st.x[(size_t)c * md.P + threadIdx.x] = xget(xv, threadIdx.x);
     }
