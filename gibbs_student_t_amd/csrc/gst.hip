@@ -442,6 +442,88 @@ static int pack_dataset(Ctx* cx, const gst_model_desc* d, gst::DevModel& md, int
     if (upload(cx, eb.data(), eb.size() * sizeof(int), &ptr)) return -1;
     md.ecb = (const int*)ptr;
   }
+  // large path, disjoint ECORR epochs: the structured Gram's operands (gst_large.hpp
+  // lg_gram_ec), when [timing model | Fourier | r | 1] fits four 16-column tiles
+  md.Tx = md.Xe = nullptr;
+  md.ekl = md.eblk = nullptr;
+  md.gx_nt = md.nkse = md.neblk = 0;
+  const int Q = ntm_pad + nf;
+  bool ec_disj = MT == 0 && nec > 0;
+  for (int t = 0; ec_disj && t < n; ++t) {
+    int nz = 0;
+    for (int e = 0; e < nec; ++e) nz += d->T[(size_t)t * m + nf + ntm + e] != 0.0;
+    ec_disj = nz <= 1;
+  }
+  if (ec_disj && Q + 2 <= 64) {
+    const int NX = (Q + 2 + 15) / 16;
+    // compact [X | r | 1] row q of TOA t (the ones column stays zero here: lg_gram_ec's G_xx
+    // does not use it)
+    auto xval = [&](int t, int q) -> double {
+      if (q < Q) return int2ref[q] >= 0 ? d->T[(size_t)t * m + int2ref[q]] : 0.0;
+      return q == Q ? d->residuals[t] : 0.0;
+    };
+    std::vector<double> tx((size_t)(npad / 4) * NX * 64, 0.0);
+    for (int ks = 0; ks < nks; ++ks)
+      for (int X = 0; X < NX; ++X)
+        for (int l = 0; l < 64; ++l) {
+          const int t = 4 * ks + (l >> 4);
+          if (t < n) tx[((size_t)ks * NX + X) * 64 + l] = xval(t, 16 * X + (l & 15));
+        }
+    // the epochs' TOAs (ascending), 16 epochs per block, each block padded to whole k-steps
+    std::vector<std::vector<int>> etoa(nec);
+    for (int t = 0; t < n; ++t)
+      for (int e = 0; e < nec; ++e)
+        if (d->T[(size_t)t * m + nf + ntm + e] != 0.0) etoa[e].push_back(t);
+    const int neblk = (nec + 15) / 16;
+    std::vector<int> eblk(neblk + 1, 0), ent_t, ent_e;
+    for (int b = 0; b < neblk; ++b) {
+      eblk[b] = (int)ent_t.size() / 4;
+      for (int e = 16 * b; e < std::min(nec, 16 * b + 16); ++e)
+        for (int t : etoa[e]) {
+          ent_t.push_back(t);
+          ent_e.push_back(e - 16 * b);
+        }
+      while (ent_t.size() % 4) {
+        ent_t.push_back(-1);
+        ent_e.push_back(-1);
+      }
+    }
+    eblk[neblk] = (int)ent_t.size() / 4;
+    const int nkse = std::max(16, round_up(eblk[neblk], 16));
+    ent_t.resize((size_t)nkse * 4, -1);
+    ent_e.resize((size_t)nkse * 4, -1);
+    std::vector<double> xe((size_t)nkse * NX * 64, 0.0);
+    std::vector<int> ekl((size_t)nkse * 8, -1);
+    for (int p = 0; p < 4 * nkse; ++p) {
+      ekl[2 * p] = ent_t[p];
+      ekl[2 * p + 1] = ent_e[p];
+    }
+    for (int b = 0; b < neblk; ++b)
+      for (int p = 4 * eblk[b]; p < 4 * eblk[b + 1]; ++p) {
+        const int t = ent_t[p];
+        if (t < 0) continue;
+        const int e = 16 * b + ent_e[p];
+        const double u = d->T[(size_t)t * m + nf + ntm + e];
+        const int ks = p / 4, k = p % 4;
+        for (int X = 0; X < NX; ++X)
+          for (int j = 0; j < 16; ++j) {
+            const int q = 16 * X + j;
+            const double v = q == Q + 1 ? u * u : u * xval(t, q);
+            xe[((size_t)ks * NX + X) * 64 + 16 * k + j] = v;
+          }
+      }
+    if (upload(cx, tx.data(), tx.size() * 8, &ptr)) return -1;
+    md.Tx = (const double*)ptr;
+    if (upload(cx, xe.data(), xe.size() * 8, &ptr)) return -1;
+    md.Xe = (const double*)ptr;
+    if (upload(cx, ekl.data(), ekl.size() * sizeof(int), &ptr)) return -1;
+    md.ekl = (const int*)ptr;
+    if (upload(cx, eblk.data(), eblk.size() * sizeof(int), &ptr)) return -1;
+    md.eblk = (const int*)ptr;
+    md.gx_nt = NX;
+    md.nkse = nkse;
+    md.neblk = neblk;
+  }
   md.lp_sum = 0.0;  // Python sum() order (gibbs.py:339)
   for (int j = 0; j < P; ++j) md.lp_sum += md.lp_in[j];
   md.nh = d->n_hyper;
@@ -835,7 +917,17 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
   for (const gst::DevModel& hm : cx->hmd)
     if (hm.mp != h.mp) gram_small = 0;
   if (gram_small > gst::GS_NTMAX || (cx->debug & GST_DEBUG_LARGE_GRAM)) gram_small = 0;
+  // datasets on the structured ECORR Gram (one tile count per batch: same structure)
+  int gram_ec_nt = 0;
+  bool gram_dense = false;
+  for (const gst::DevModel& hm : cx->hmd) {
+    if (gst::gram_ec_of(hm, hyper_lds, cx->debug))
+      gram_ec_nt = hm.gx_nt;
+    else
+      gram_dense = true;
+  }
   const dim3 g_gs((C + gst::GS_WPB - 1) / gst::GS_WPB), b_gs(64 * gst::GS_WPB);
+  const dim3 g_gec((C + gst::GEC_CPB - 1) / gst::GEC_CPB);
   const dim3 g_chain(C), b_chain(gst::LBLK);
   const dim3 g_gram(npairs * ((C + gst::GRAM_WAVES - 1) / gst::GRAM_WAVES)), b_gram(64 * gst::GRAM_WAVES);
   const dim3 g_tb(ys / 64, (C + 64 * gst::TB_CG - 1) / (64 * gst::TB_CG));
@@ -861,7 +953,16 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
     }
     if ((mask & (6u | GST_STAGE_GRAM)) || eval_only) {
       if (ev_mark(cx, GST_K_GRAM, st, true)) return -1;
-      switch (gram_small) {
+      // the structured Gram for the datasets it takes (gram_ec_of), the dense one for the
+      // rest (each skips the other's chains)
+      switch (gram_ec_nt) {
+        case 1: hipLaunchKernelGGL(gst::lg_gram_ec<1>, g_gec, b_gs, 0, st, cx->dmd, a); break;
+        case 2: hipLaunchKernelGGL(gst::lg_gram_ec<2>, g_gec, b_gs, 0, st, cx->dmd, a); break;
+        case 3: hipLaunchKernelGGL(gst::lg_gram_ec<3>, g_gec, b_gs, 0, st, cx->dmd, a); break;
+        case 4: hipLaunchKernelGGL(gst::lg_gram_ec<4>, g_gec, b_gs, 0, st, cx->dmd, a); break;
+        default: break;
+      }
+      if (gram_dense) switch (gram_small) {
         case 1: hipLaunchKernelGGL(gst::lg_gram_small<1>, g_gs, b_gs, 0, st, cx->dmd, a); break;
         case 2: hipLaunchKernelGGL(gst::lg_gram_small<2>, g_gs, b_gs, 0, st, cx->dmd, a); break;
         case 3: hipLaunchKernelGGL(gst::lg_gram_small<3>, g_gs, b_gs, 0, st, cx->dmd, a); break;

@@ -132,6 +132,16 @@ struct DevModel {
   int ec_disjoint;          // every TOA in at most one ECORR column (the batch's datasets all)
   const int* ecb;           // [nec] backend of each ECORR column
   double ec_count[NBMAX];   // ECORR columns per backend
+  // large path, disjoint ECORR epochs (gst_large.hpp lg_gram_ec; gx_nt = 0: not built): the
+  // Gram's X part (timing model + Fourier + r + a ones column, gx_nt 16-column tiles) packed
+  // as Tmf, and the epochs' TOAs in epoch order, 16 epochs per block, each block padded to
+  // whole k-steps of 4: their X rows times the ECORR basis value ([nkse][gx_nt][64]), TOA
+  // index and block-local epoch of each entry ([nkse * 4][2], -1 padding), block k-step starts
+  const double* Tx;
+  const double* Xe;
+  const int* ekl;
+  const int* eblk;          // [neblk + 1]
+  int gx_nt, nkse, neblk;
   double sig_h, sig_w;
   double mh_cdf[5], mh_size[5];
   int model, vary_df, vary_alpha;
@@ -315,6 +325,7 @@ constexpr double FLOOR_GATE = 0x1p-52;
 constexpr double FLOOR_C = GST_FLOOR_C;
 constexpr int STATUS_FLOOR = 16;
 constexpr int STATUS_FLOOR_COUNT = 256;   // one floor draw, counted in bits 8..30
+constexpr int DEBUG_LARGE_GRAM = 2;    // large path: dense super-tile Gram (lg_gram) forced
 constexpr int DEBUG_EXACT_BDRAW = 8;
 constexpr int DEBUG_MFMA_GRAM = 16;   // persistent kernel: no low-rank Gram (tests, A/B)
 constexpr int DEBUG_EPOCHS_LDS = 32;  // large path: ECORR-epochs-first chains on lg_hyper<2>

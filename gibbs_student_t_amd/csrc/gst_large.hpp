@@ -104,12 +104,22 @@ __host__ __device__ constexpr int ec_reg_mt(int hclass, int ntm, int nf, int nec
 __host__ __device__ inline int ec_reg_mt_of(const DevModel& md, int force_lds, int debug) {
   return ec_reg_mt(hyper_class_of(md, force_lds), md.ntm, md.nf, md.nec, debug);
 }
+// Chains whose dataset has disjoint ECORR epochs and runs them epochs first (class 2) take the
+// structured Gram lg_gram_ec (DevModel::gx_nt > 0), which computes only the blocks class 2 reads:
+// G_xx (X = timing model, Fourier, r), the epochs' diagonal and their couplings to X.  The
+// dense Grams (lg_gram, lg_gram_small) skip these chains.  GST_DEBUG_LARGE_GRAM: dense.
+__host__ __device__ inline bool gram_ec_of(const DevModel& md, int force_lds, int debug) {
+  return md.gx_nt > 0 && !(debug & DEBUG_LARGE_GRAM) && hyper_class_of(md, force_lds) == 2;
+}
 constexpr int GRAM_WAVES = 8;  // chains per gram workgroup
 #ifndef GST_TM_PW
 #define GST_TM_PW 16   // A/B builds override it (32: config-5 tmelim 1.75 -> 2.95 ms, ebig -20%)
 #endif
 constexpr int TM_PW = GST_TM_PW;   // panel width of the blocked eliminations (panel_ldl)
-constexpr int TM_TILES = 4;   // trailing-update tiles per wave per round (lg_tmelim)
+#ifndef GST_TM_TILES
+#define GST_TM_TILES 4   // (8: measured no faster on config 5, round 6)
+#endif
+constexpr int TM_TILES = GST_TM_TILES;   // trailing-update tiles per wave per round (panel_ldl)
 
 struct LScratch {
   double* G;   // [C][mp*mp] Gram (row-major, lower triangle); kept for the floor pass
@@ -808,6 +818,7 @@ __global__ void __launch_bounds__(64 * GRAM_WAVES) lg_gram(const DevModel* __res
   // the group's dataset (its first chain's): every wave stages that dataset's T
   const int dsg = ds_of(a, (blockIdx.x % ngroups) * GRAM_WAVES);
   const DevModel& md = mds[dsg];
+  if (gram_ec_of(md, a.hyper_lds, a.st.debug)) return;   // the group's Gram is lg_gram_ec's
   if (live && prank == 0 && ds_of(a, c) != dsg && (threadIdx.x & 63) == 0 && a.st.status)
     a.st.status[c] |= 8;                          // batch layout violated: flag, never silent
   const int noff = npairs - nsb;
@@ -858,6 +869,7 @@ __global__ void __launch_bounds__(64 * GS_WPB) lg_gram_small(const DevModel* __r
   const int c = blockIdx.x * GS_WPB + (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (c >= a.C) return;
   const DevModel& md = mds[ds_of(a, c)];
+  if (gram_ec_of(md, a.hyper_lds, a.st.debug)) return;   // lg_gram_ec's chain
   const int tl = lane >> 4, nks = md.npad / 4, mp = md.mp;
   const GDouble* wc = (const GDouble*)(a.s.w + (size_t)c * a.ys);
   const GDouble* Tm = (const GDouble*)md.Tmf;
@@ -913,6 +925,158 @@ __global__ void __launch_bounds__(64 * GS_WPB) lg_gram_small(const DevModel* __r
 #pragma unroll
       for (int g = 0; g < 4; ++g)
         Gc[(size_t)(16 * I + tl + 4 * g) * mp + 16 * J + (lane & 15)] = acc[I * (I + 1) / 2 + J][g];
+}
+
+// ------------------------------------------------------------------------------------
+// gram, disjoint ECORR epochs (hyper class 2): only the blocks the epochs-first elimination
+// reads.  With X = [timing model | Fourier] (internal columns 0 .. Q-1), r and the epoch
+// columns E (each TOA in at most one epoch, value u_t):
+//   G_xx = [X|r]^T W [X|r]       one wave's MFMA tiles over the compact packed [X | r | 1]
+//   G_ee = sum_{t in e} w_t u_t^2,   G_ex = sum_{t in e} w_t u_t [X|r]_t
+// the second pair as MFMAs too: per block of 16 epochs, A = the 16 x 4 indicator of which
+// epoch each of 4 consecutive (epoch-ordered) TOAs belongs to, B = their w u [X | r | u] rows,
+// accumulating the block's 16 rows of [G_ex | G_er | G_ee].  O(n (Q + 2)^2 / 2) MFMA work per
+// chain instead of the dense Gram's O(n mp^2 / 2) (gibbs.py:302-304; the E-E off-diagonal
+// blocks are exactly zero and never read).  Two waves per chain: G_xx and the epochs' blocks
+// (their MFMAs share the SIMD's pipe; the second wave hides the first's load latency).
+// ------------------------------------------------------------------------------------
+constexpr int GEC_CPB = GS_WPB / 2;   // chains per lg_gram_ec workgroup
+template <int NX>
+__global__ void __launch_bounds__(64 * GS_WPB) lg_gram_ec(const DevModel* __restrict__ mds,
+                                                            LArgs a) {
+  constexpr int NXT = NX * (NX + 1) / 2;
+  const int lane = threadIdx.x & 63;
+  const int wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = blockIdx.x * GEC_CPB + (wv >> 1), role = wv & 1;
+  if (c >= a.C) return;
+  const DevModel& md = mds[ds_of(a, c)];
+  if (!gram_ec_of(md, a.hyper_lds, a.st.debug) || md.gx_nt != NX) return;
+  const int tl = lane >> 4, mp = md.mp, Q = md.ntm_pad + md.nf, raug = md.raug;
+  const int ec0 = md.ntm_pad + md.nf;   // internal column of epoch 0
+  const GDouble* wc = (const GDouble*)(a.s.w + (size_t)c * a.ys);
+  double* Gc = a.s.G + (size_t)c * mp * mp;
+  constexpr int D = GS_DEPTH;
+  // ---- G_xx: lg_gram_small's loop over the compact columns
+  if (role == 0) {
+    const GDouble* Tm = (const GDouble*)md.Tx;
+    const int nks = md.npad / 4;
+    v4d acc[NXT];
+#pragma unroll
+    for (int i = 0; i < NXT; ++i) acc[i] = (v4d){0.0, 0.0, 0.0, 0.0};
+    double t[D][NX], w[D];
+    auto tload = [&](double (&tt)[NX], double& ww, int ks) __attribute__((always_inline)) {
+#pragma unroll
+      for (int X = 0; X < NX; ++X) tt[X] = Tm[((size_t)ks * NX + X) * 64 + lane];
+      ww = wc[4 * ks + tl];
+    };
+    auto kstep = [&](const double (&tt)[NX], const double wt) __attribute__((always_inline)) {
+#pragma unroll
+      for (int I = 0; I < NX; ++I) {
+        const double av = tt[I] * wt;
+#pragma unroll
+        for (int J = 0; J <= I; ++J)
+          acc[I * (I + 1) / 2 + J] =
+              __builtin_amdgcn_mfma_f64_16x16x4f64(av, tt[J], acc[I * (I + 1) / 2 + J], 0, 0, 0);
+      }
+    };
+    static_assert(16 % D == 0, "k-step count is a multiple of 16");
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      tload(t[d], w[d], d);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    int ks = 0;
+    for (; ks + D < nks; ks += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        kstep(t[d], w[d]);
+        tload(t[d], w[d], ks + d + D);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) kstep(t[d], w[d]);
+    // compact column q -> internal: q < Q itself, Q the residual row, Q + 1 (ones) unused
+#pragma unroll
+    for (int I = 0; I < NX; ++I)
+#pragma unroll
+      for (int J = 0; J <= I; ++J)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int qa = 16 * I + tl + 4 * g, qb = 16 * J + (lane & 15);
+          if (qa >= qb && qa <= Q && qb <= Q) {
+            const int gi = qa < Q ? qa : raug, gj = qb < Q ? qb : raug;
+            Gc[(size_t)gi * mp + gj] = acc[I * (I + 1) / 2 + J][g];
+          }
+        }
+  }
+  // ---- epochs: blocks of 16, A = indicator (lane: row = lane & 15, k = lane >> 4),
+  // B = w_t u_t [X | r | u]_t (lane: k = lane >> 4, column = lane & 15)
+  if (role == 1) {
+    const GDouble* Xe = (const GDouble*)md.Xe;
+    const int* ekl = md.ekl;
+    const int nks = md.nkse;
+    v4d acc[NX];
+#pragma unroll
+    for (int v = 0; v < NX; ++v) acc[v] = (v4d){0.0, 0.0, 0.0, 0.0};
+    double xb[D][NX], ind[D];
+    auto eload = [&](int d, int ks) __attribute__((always_inline)) {
+      const int p = 4 * ks + tl;
+      const int tt = ekl[2 * p], el = ekl[2 * p + 1];
+      const double wt = tt >= 0 ? (double)wc[tt] : 0.0;
+      ind[d] = el == (lane & 15) ? 1.0 : 0.0;
+#pragma unroll
+      for (int v = 0; v < NX; ++v) xb[d][v] = Xe[((size_t)ks * NX + v) * 64 + lane] * wt;
+    };
+    auto flush = [&](int blk) __attribute__((always_inline)) {
+#pragma unroll
+      for (int v = 0; v < NX; ++v) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int e = 16 * blk + tl + 4 * g, q = 16 * v + (lane & 15);
+          if (e < md.nec) {
+            const int ge = ec0 + e;
+            if (q < Q)
+              Gc[(size_t)ge * mp + q] = acc[v][g];
+            else if (q == Q)
+              Gc[(size_t)raug * mp + ge] = acc[v][g];
+            else if (q == Q + 1)
+              Gc[(size_t)ge * mp + ge] = acc[v][g];
+          }
+        }
+        acc[v] = (v4d){0.0, 0.0, 0.0, 0.0};
+      }
+    };
+    static_assert(16 % D == 0, "k-step count is a multiple of 16");
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      eload(d, d);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    int blk = 0, kend = md.eblk[1];
+    int ks = 0;
+    auto estep = [&](int d, int k) __attribute__((always_inline)) {
+      while (k == kend) {              // (wave-uniform) the block's k-steps are done
+        if (blk < md.neblk) flush(blk);
+        ++blk;
+        kend = blk < md.neblk ? md.eblk[blk + 1] : 0x7fffffff;
+      }
+#pragma unroll
+      for (int v = 0; v < NX; ++v)
+        acc[v] = __builtin_amdgcn_mfma_f64_16x16x4f64(ind[d], xb[d][v], acc[v], 0, 0, 0);
+    };
+    for (; ks + D < nks; ks += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        estep(d, ks + d);
+        eload(d, ks + d + D);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) estep(d, ks + d);
+    if (blk < md.neblk) flush(blk);
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -2369,7 +2533,10 @@ __global__ void __launch_bounds__(LBLK) lg_btm(const DevModel* __restrict__ mds,
 // k-steps of operands in flight.  Every y element receives the same MFMA sequence (k in
 // order, the same A / B values) whatever CG is, so y is bitwise that of one group per wave.
 constexpr int TB_CG = 4;      // 16-chain groups per wave (chains per wave: 64)
-constexpr int TB_DEPTH = 2;   // k-steps of operands in flight
+#ifndef GST_TB_DEPTH
+#define GST_TB_DEPTH 2   // (3: measured no faster on config 5, round 6)
+#endif
+constexpr int TB_DEPTH = GST_TB_DEPTH;   // k-steps of operands in flight
 template <int CG>
 __device__ __forceinline__ void tb_tile(const DevModel& md, const LArgs& a, int t0, int cb) {
   const int lane = threadIdx.x & 63;
