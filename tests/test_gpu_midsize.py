@@ -275,6 +275,23 @@ def test_register_epochs_first_matches_lds_epochs_first(name):
     1e-10 at 256 states (prior draws, the fixture's latents) and 16 chains x 6 sweeps from
     the fixture's start make the same MH, z and nu decisions with b, alpha, pout, theta within
     1e-8 relative."""
+    _compare_large_variants(name, {}, {"epochs_lds": True})
+
+
+@pytest.mark.parametrize("name", ["ebig_beta_fixed", "ebig_t_fixed", "mb_beta_fixed",
+                                  "mb_t_fixed", "mbn_vvh17_fixed"])
+def test_structured_ecorr_gram_matches_dense_gram(name):
+    """lg_gram_ec (round 6: for disjoint ECORR epochs run epochs first, only G_xx, the epochs'
+    diagonal and their couplings to [timing model | Fourier | r], by MFMA over the compact
+    columns and over the epoch-ordered TOAs) against the dense Gram (GST_DEBUG_LARGE_GRAM:
+    lg_gram / lg_gram_small over all mp columns): the same hyper kernel on Grams that differ
+    in summation order only, held to the tolerances of the two eliminations above."""
+    _compare_large_variants(name, {}, {"large_gram": True})
+
+
+def _compare_large_variants(name, dbg_a, dbg_b):
+    """Likelihoods at 256 states and 16 chains x 6 sweeps of two large-path builds of the same
+    chain (debug flags dbg_a, dbg_b) from the fixture's start."""
     if not torch.cuda.is_available():
         pytest.skip("needs a HIP device")
     from golden_io import load_ref, sweep_state
@@ -286,9 +303,9 @@ def test_register_epochs_first_matches_lds_epochs_first(name):
     hi = np.array([p.pmax for p in pta.params])
     x = np.random.default_rng(12).uniform(lo, hi, size=(C2, len(lo)))
     got, outs = [], []
-    for lds in (False, True):
+    for dbg in (dbg_a, dbg_b):
         ns = NativeSampler(pta, ref["kw"], 0, path="large")
-        ns.set_debug(epochs_lds=lds)
+        ns.set_debug(**dbg)
         ns.alloc(C2)
         ns.set_state(x=x, b=np.tile(s0["b"], (C2, 1)), z=np.tile(s0["z"], (C2, 1)),
                      alpha=np.tile(s0["alpha"], (C2, 1)), pout=np.tile(s0["pout"], (C2, 1)),
@@ -296,7 +313,7 @@ def test_register_epochs_first_matches_lds_epochs_first(name):
         got.append(ns.eval_lnlike())
         ns.close()
         ns = NativeSampler(pta, ref["kw"], 0, path="large")
-        ns.set_debug(epochs_lds=lds)
+        ns.set_debug(**dbg)
         ns.alloc(C)
         ns.set_state(x=np.tile(ref["xs"], (C, 1)), b=np.tile(s0["b"], (C, 1)),
                      z=np.tile(s0["z"], (C, 1)), alpha=np.tile(s0["alpha"], (C, 1)),
