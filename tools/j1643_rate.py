@@ -9,6 +9,10 @@ observation) and times chain-sweeps on the large path, with the structured ECORR
 (lg_gram_ec, the default) and with the dense one (GST_DEBUG_LARGE_GRAM).
 
     python tools/j1643_rate.py [chains] [sweeps]
+    python tools/j1643_rate.py --cpu [seconds]   # the reference algorithm on one CPU core
+
+(--cpu: oracle/gibbs_oracle.py, the line-cited restatement of gibbs.py that reproduces its
+chains bit for bit, with numpy's legacy RNG calls -- as the test-infrastructure CPU baseline.)
 """
 import json
 import sys
@@ -51,7 +55,33 @@ def rate(pta, C, S, **debug):
             "status_clean": bool(np.all((st & 0xef) == 0))}
 
 
+def cpu_rate(seconds):
+    import os
+    import time
+    import warnings
+    os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")
+    from oracle.gibbs_oracle import LegacyNumpyVariates, Oracle, OutlierModel, initial_state
+    warnings.simplefilter("ignore")
+    pta = j1643_like()
+    orc = Oracle(pta, OutlierModel(**MODELS["vvh17"]))
+    st = initial_state(pta, orc.cfg)
+    np.random.seed(5)
+    x = np.array(pta.sample_params(), dtype=np.float64)
+    src = LegacyNumpyVariates()
+    x = orc.sweep(st, x, src)    # (first sweep: caches and page-in)
+    t0, k = time.perf_counter(), 0
+    while time.perf_counter() - t0 < seconds:
+        x = orc.sweep(st, x, src)
+        k += 1
+    dt = time.perf_counter() - t0
+    return {"dataset": "j1643-like", "cpu": "oracle (reference algorithm), 1 core",
+            "sweeps": k, "seconds": dt, "sweeps_per_s": k / dt}
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--cpu":
+        print(json.dumps(cpu_rate(float(sys.argv[2]) if len(sys.argv) > 2 else 20.0)))
+        return
     C = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
     S = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     pta = j1643_like()
