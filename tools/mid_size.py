@@ -28,14 +28,17 @@ def rate(pta, C, S, path):
     ns.sweep(S, seed=1, sweep0=20)
     ns.synchronize()
     ms = ns.last_kernel_ms() if path == "persistent" else None
+    stages = None
     if ms is None:
         ns.set_timing(True)
         ns.sweep(S, seed=1, sweep0=20 + S)
         ns.synchronize()
-        ms = sum(v[0] for v in ns.kernel_times().values())
+        kt = ns.kernel_times()
+        ms = sum(v[0] for v in kt.values())
+        stages = {k: round(v[0] / S, 4) for k, v in kt.items() if v[1]}
     ok = bool(np.all((ns.get_state()["status"] & 0xef) == 0))   # floor draws are not errors
     ns.close()
-    return C * S / (ms * 1e-3), ms / S, ok
+    return C * S / (ms * 1e-3), ms / S, ok, stages
 
 
 def main():
@@ -52,9 +55,11 @@ def main():
         psr = data.multiband(nepochs=nepochs, nsub=nsub, seed=7)
         pta = PTA(psr)
         for path in paths:
-            r, ms, ok = rate(pta, C, S if path == "persistent" else max(2, S // 10), path)
+            r, ms, ok, stages = rate(pta, C, S if path == "persistent" else max(2, S // 10), path)
             row = {"n": pta.n, "path": path, "chain_sweeps_per_s": r, "ms_per_sweep": ms,
                    "status_clean": ok}
+            if stages:
+                row["stages_ms_per_sweep"] = stages
             out["rows"].append(row)
             print(json.dumps(row), flush=True)
     if len(sys.argv) > 3:
