@@ -920,6 +920,10 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
   // datasets on the structured ECORR Gram (one tile count per batch: same structure)
   int gram_ec_nt = 0;
   bool gram_dense = false;
+  // lg_tmelim and lg_btm return at once for class-2 chains (the epochs-first kernels factor the
+  // timing model and draw all of b): a batch of class-2 datasets does not launch them
+  bool tm_needed = false;
+  for (const gst::DevModel& hm : cx->hmd) tm_needed = tm_needed || gst::hyper_class_of(hm, hyper_lds) != 2;
   for (const gst::DevModel& hm : cx->hmd) {
     if (gst::gram_ec_of(hm, hyper_lds, cx->debug))
       gram_ec_nt = hm.gx_nt;
@@ -976,7 +980,7 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
       HIP_OK(hipGetLastError());
       if (ev_mark(cx, GST_K_GRAM, st, false)) return -1;
       if (!eval_only) cx->gram_large += (unsigned long long)C;
-      LG_LAUNCH(GST_K_TMELIM, gst::lg_tmelim, g_chain, b_chain, cx->lds_tm);
+      if (tm_needed) LG_LAUNCH(GST_K_TMELIM, gst::lg_tmelim, g_chain, b_chain, cx->lds_tm);
       if (!(mask & GST_STAGE_GRAM)) {   // timing diagnostic: Gram + TM elimination only
         if (launch_hyper(cx, a, hcls, g_hr8, b_hr8, g_hr16, b_hr16, g_chain, b_chain, st))
           return -1;
@@ -986,13 +990,13 @@ static int launch_large(Ctx* cx, const gst::DevState& ds, const gst::DevRec& dr,
           // fp64 resolution re-eliminate G with Sigma + f I and draw there; every other chain
           // returns at once (SC_FLOOR == 0)
           a.floor_pass = 1;
-          LG_LAUNCH(GST_K_TMELIM, gst::lg_tmelim, g_chain, b_chain, cx->lds_tm);
+          if (tm_needed) LG_LAUNCH(GST_K_TMELIM, gst::lg_tmelim, g_chain, b_chain, cx->lds_tm);
           if (launch_hyper(cx, a, hcls, g_hr8, b_hr8, g_hr16, b_hr16, g_chain, b_chain, st))
             return -1;
           a.floor_pass = 0;
         }
         if (mask & 4u) {
-          LG_LAUNCH(GST_K_BTM, gst::lg_btm, g_chain, b_chain, cx->lds_btm);
+          if (tm_needed) LG_LAUNCH(GST_K_BTM, gst::lg_btm, g_chain, b_chain, cx->lds_btm);
           LG_LAUNCH(GST_K_TB, gst::lg_tb, g_tb, b_chain, 0);
         }
       }
