@@ -247,7 +247,10 @@ int gst_set_waves(void* ctx, int waves);
  * with this flag must give bitwise the same chains as one without (a read of any stale word
  * would surface as NaN / different draws).  Costs time; never set in production. */
 /* Large path: GST_DEBUG_LARGE_GRAM forces the 64x64 super-tile Gram (lg_gram) where the
- * one-wave-per-chain Gram (lg_gram_small) would run; the two give bitwise the same G.
+ * one-wave-per-chain Gram (lg_gram_small) would run; the two give bitwise the same G.  It also
+ * turns off the structured ECORR Gram (lg_gram_ec, round 6: disjoint ECORR epochs eliminated
+ * first -- only G_xx, the epochs' diagonal and their couplings, by MFMA), whose G blocks agree
+ * with the dense Gram's to rounding (summation order). */
  * GST_DEBUG_LARGE_HYPER forces the LDS-resident hyper kernel (lg_hyper) where the register-
  * resident one (lg_hyper_reg) would run: same variates and decisions, likelihoods within
  * rounding; and the blocked global-memory elimination (lg_hyper<1>) where the ECORR-epochs-
