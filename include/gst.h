@@ -235,9 +235,8 @@ int gst_get_path(void* ctx, int* path);
  * that split the red-noise MH block's likelihood evaluations (AUTO, the default); the
  * chain's draws are bitwise those of the one-wave kernel.  GST_WAVES_ONE / GST_WAVES_TWO
  * force either kernel for every sampling launch (tape-mode and gst_eval_lnlike launches
- * always run one wave per chain).  The general white-noise model has no two-wave kernel: AUTO
- * runs it on one wave, and a sampling launch (gst_sweep without a tape) with GST_WAVES_TWO
- * set fails; its tape-mode and gst_eval_lnlike launches run one wave as for every model. */
+ * always run one wave per chain).  Since round 6 the general white-noise model (per-backend
+ * white noise, ECORR columns) has the two-wave kernel too. */
 enum gst_waves { GST_WAVES_AUTO = 0, GST_WAVES_ONE = 1, GST_WAVES_TWO = 2 };
 int gst_set_waves(void* ctx, int waves);
 
@@ -250,7 +249,7 @@ int gst_set_waves(void* ctx, int waves);
  * one-wave-per-chain Gram (lg_gram_small) would run; the two give bitwise the same G.  It also
  * turns off the structured ECORR Gram (lg_gram_ec, round 6: disjoint ECORR epochs eliminated
  * first -- only G_xx, the epochs' diagonal and their couplings, by MFMA), whose G blocks agree
- * with the dense Gram's to rounding (summation order). */
+ * with the dense Gram's to rounding (summation order).
  * GST_DEBUG_LARGE_HYPER forces the LDS-resident hyper kernel (lg_hyper) where the register-
  * resident one (lg_hyper_reg) would run: same variates and decisions, likelihoods within
  * rounding; and the blocked global-memory elimination (lg_hyper<1>) where the ECORR-epochs-

@@ -61,3 +61,17 @@ def test_model_desc_packing():
 def test_missing_library_raises(tmp_path):
     with pytest.raises(_abi.GstNativeError):
         _abi.load(str(tmp_path / "nope.so"))
+
+
+def test_header_is_valid_c():
+    """include/gst.h compiles as C on its own (a C / cgo / ctypes consumer includes it bare)."""
+    import shutil
+    import subprocess
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    hdr = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                       "gst.h")
+    r = subprocess.run([cc, "-fsyntax-only", "-Wall", "-Werror", "-x", "c", hdr],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
