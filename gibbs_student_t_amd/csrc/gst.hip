@@ -1047,12 +1047,9 @@ static int launch(Ctx* cx, const gst_state* s, const gst_records* r, const gst_t
     if (wpb >= 1 && C <= cx->ncu) wpb = 1;
     else if (wpb >= 2 && C <= 2 * cx->ncu) wpb = 2;
   }
-  // two waves per chain when every chain would otherwise leave a SIMD idle
-  // (not for the general white-noise model: its instances run one wave per chain)
-  if (cx->gen && cx->waves == GST_WAVES_TWO && !tape && !eval_only)
-    return fail("gst: two waves per chain are not built for the general white-noise model "
-                "(per-backend white noise / ECORR); use GST_WAVES_AUTO or GST_WAVES_ONE");
-  const bool pair = !cx->gen && !tape && !eval_only && !(mask & GST_STAGE_GRAM) &&
+  // two waves per chain when every chain would otherwise leave a SIMD idle (the general
+  // white-noise instances too, since round 6)
+  const bool pair = !tape && !eval_only && !(mask & GST_STAGE_GRAM) &&
                     (cx->waves == GST_WAVES_TWO || (cx->waves == GST_WAVES_AUTO && C <= 2 * cx->ncu));
   kfn_t k = pick(cx->MT, cx->NS, cx->K0, cx->raug, cx->gen, tape, wpb,
                  C > 4 * cx->ncu && cx->NS <= gst::OCC2_NS_MAX, pair);

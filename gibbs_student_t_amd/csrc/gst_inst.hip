@@ -17,11 +17,11 @@ kfn_t kfn() {
   return &gst_sweep_kernel<MT, NS, K0, RA, TAPE, WPB, OCC, PAIR, GEN>;
 }
 
-// GEN shapes (the general white-noise model): no pair mode (the host never asks for it)
+// GEN shapes: the general white-noise model (pair mode since round 6)
 template <int MT, int NS, int K0, int RA, int GEN>
 kfn_t pick_shape(bool tape, int wpb, bool occ2, bool pair) {
   if constexpr (GEN != 0) {
-    if (pair) return nullptr;
+    if (pair && !tape) return kfn<MT, NS, K0, RA, false, 2, 1, true, true>();
     if (tape) return kfn<MT, NS, K0, RA, true, 4, 1, false, true>();
     if (wpb == 1) return kfn<MT, NS, K0, RA, false, 1, 1, false, true>();
     if (wpb == 2) return kfn<MT, NS, K0, RA, false, 2, 1, false, true>();

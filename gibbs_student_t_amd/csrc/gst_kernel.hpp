@@ -1007,7 +1007,7 @@ __device__ __forceinline__ void chol_stats(CholCtx& cc) {
 // -- and exchange the lnL values through LDS, so that a round settles one or two MH steps
 // (DESIGN.md section 8).
 // GEN: the general white-noise model (per-backend efac / equad, ECORR epoch columns in the
-// hyper block, up to 8 parameters; gibbs.py:64-77) -- no pair mode.
+// hyper block, up to 8 parameters; gibbs.py:64-77); pair mode too since round 6.
 template <int MT, int NS, int K0, int RA, bool TAPE, int WPB = 4, int OCC = 1, bool PAIR = false,
           bool GEN = false>
 __global__ void __launch_bounds__(64 * WPB, OCC)
@@ -1016,7 +1016,6 @@ __global__ void __launch_bounds__(64 * WPB, OCC)
                      unsigned long long seed, long long chain0, int eval_only, double* out_w,
                      double* out_h) {
   static_assert(!PAIR || (WPB == 2 && !TAPE), "pair mode: one chain per 2-wave workgroup");
-  static_assert(!GEN || !PAIR, "general white noise: one wave per chain");
   constexpr int PX = GEN ? 8 : 4;     // parameters held in registers
   constexpr int NSL = SL(MT, 0);
   constexpr int NT = MT / 2;          // 16-wide MFMA tiles

@@ -24,14 +24,13 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 # (+ the general white-noise instances: two backends with ECORR, one backend with ECORR,
-# J1713+0747 with two backends and no ECORR; these have no two-waves-per-chain build)
+# J1713+0747 with two backends and no ECORR; two waves per chain for them since round 6)
 FIXTURES = ("beta_efac_fixed", "c3_beta_fixed", "tm22_beta_fixed", "vvh17_prior",
             "ecb_beta_fixed", "ecq_t_fixed", "jb_uniform_fixed")
 
 
 def _skip_pair(name, build):
-    if build == "pair" and name.startswith(("ec", "jb")):
-        pytest.skip("general white-noise model: one wave per chain only")
+    """(round 5: the general white-noise instances had no pair build; they have since round 6)"""
 
 
 def _ncu():

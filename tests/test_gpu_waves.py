@@ -44,7 +44,10 @@ def _run(ref, C, S, waves, init, mask=_abi.STAGE_ALL, seed=7, sweep0=3, chain0=0
 # every model family, the efac-varied fixture, the 5%-outlier simulate_data pulsar, and
 # the two other register shapes (20 components: MT = 8; 22 timing-model columns: K0 = 3)
 FIXTURES = ("beta_prior", "t_prior", "gaussian_prior", "uniform_prior", "vvh17_prior",
-            "beta_efac_fixed", "c3_beta_fixed", "c20_t_fixed", "tm22_beta_fixed")
+            "beta_efac_fixed", "c3_beta_fixed", "c20_t_fixed", "tm22_beta_fixed",
+            # the general white-noise instances (round 6): two backends + ECORR, one backend +
+            # ECORR, J1713+0747 with two backends
+            "ecb_beta_fixed", "ecq_t_fixed", "jb_uniform_fixed")
 
 
 @pytest.mark.parametrize("name", FIXTURES)
